@@ -1,0 +1,157 @@
+/*
+ * mgx.h -- C ABI of the MI355X-native vectorised MiniGrid engine (libmgx.so).
+ *
+ * Drop-in boundary.  The reference reaches this path through Python objects,
+ * not an FFI; each entry point below replaces one of them:
+ *
+ *   mgx_create   <- make_vec_env(make_env, n_envs, seed, SubprocVecEnv)  src/ppo.py:118-122
+ *                   + PlaygroundEnv.__init__                              src/custom_env.py:74-116
+ *                   + VecTransposeImage / VecFrameStack(n_stack,'first')  src/ppo.py:124-126
+ *   mgx_reset    <- VecEnv.reset() -> env_i.reset(seed=seed+i)
+ *                   -> PlaygroundEnv._gen_grid                            src/custom_env.py:122-267
+ *                   -> TokenizeVocabWrapper / Discrete2BoxWrapper         src/environment.py:69-149
+ *   mgx_step     <- VecEnv.step(actions): PlaygroundEnv.step              src/custom_env.py:269-330
+ *                   + SubprocVecEnv auto-reset, Monitor episode stats,
+ *                   terminal_observation, TimeLimit.truncated (SB3, via ppo.py:159)
+ *   mgx_gae      <- DictRolloutBuffer.compute_returns_and_advantage (SB3, via ppo.py:159)
+ *   mgx_destroy  <- VecEnv.close()                                        src/ppo.py:169
+ *
+ * Conventions: plain C, no exceptions cross the ABI; every call returns an
+ * mgx_status (0 = OK) and mgx_last_error() describes the last failure of the
+ * calling thread.  All buffers named *_dev are caller-owned DEVICE pointers
+ * (e.g. torch.Tensor.data_ptr()); `stream` is a hipStream_t (NULL = default).
+ * mgx_reset / mgx_step / mgx_gae only enqueue work on `stream` (no host sync,
+ * no allocation) and are therefore hipGraph-capturable.  A handle is not
+ * thread-safe; use one handle per device (per rank).
+ */
+#ifndef MGX_H_
+#define MGX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGX_ABI_VERSION 1
+
+/* Live-lock cap (engine policy; the reference hangs): a
+ * reset attempt may consume at most this many MT19937 words; the attempt that
+ * would take one more is abandoned and the reset re-runs unseeded with both
+ * RNG streams continuing. */
+#define MGX_LIVELOCK_WORDS 4096
+
+typedef enum {
+    MGX_OK = 0,
+    MGX_ERR_INVALID = 1,      /* bad argument / unsupported configuration */
+    MGX_ERR_HIP = 2,          /* a HIP runtime call failed */
+    MGX_ERR_DEVICE = 3,       /* the device reported an error (see mgx_poll_error) */
+    MGX_ERR_OOM = 4
+} mgx_status;
+
+/* PlaygroundEnv problems (custom_env.py:134-152) */
+typedef enum {
+    MGX_PROBLEM_MULTI = 0, MGX_PROBLEM_FULL = 1, MGX_PROBLEM_GTO = 2, MGX_PROBLEM_GTG = 3,
+    MGX_PROBLEM_OPN = 4, MGX_PROBLEM_PKP = 5, MGX_PROBLEM_DRP = 6, MGX_PROBLEM_MOV = 7
+} mgx_problem;
+
+/* which done envs get a stacked terminal observation written */
+typedef enum { MGX_TERMINAL_NONE = 0, MGX_TERMINAL_TRUNCATED = 1, MGX_TERMINAL_ALL = 2 } mgx_terminal_mode;
+
+/* Device error bits reported by mgx_poll_error */
+#define MGX_DEVERR_MT_TABLE   1u   /* an env ran past the MT19937 output table */
+#define MGX_DEVERR_BAD_ACTION 2u   /* action outside 0..6 (minigrid raises ValueError) */
+#define MGX_DEVERR_PCG_LOOP   4u   /* a PCG64 rejection loop exceeded its safety bound */
+#define MGX_DEVERR_OBJECTS    8u   /* generator ran out of objects (AssertionError in the reference) */
+
+typedef struct mgx_config {
+    int32_t problem;           /* mgx_problem; `env.problem` */
+    int32_t mission;           /* `env.mission`: 0 'go to', 1 'toggle', 2 'pick up', 5 'go to goal'; -1 = None */
+    int32_t size;              /* `env.size` (5..16); max_steps = size^2 (custom_env.py:114) */
+    int32_t num_objects;       /* `env.num_objects` */
+    int32_t see_through_walls; /* must be 1 (process_vis path not built) */
+    int32_t all_doors_open;    /* `env.all_doors_open` */
+    int32_t obstacles;         /* must be 0 (every shipped config) */
+    int32_t n_stack;           /* `algorithm.n_frames_stack` (1..8) */
+    int64_t n_envs;            /* envs owned by this handle */
+    int64_t base_seed;         /* `seed`; env i: PCG64(SeedSequence(base_seed + env_index_offset + i)), MT19937(base_seed) */
+    int64_t env_index_offset;  /* global index of env 0 (rank * n_envs when sharding) */
+    int32_t livelock_words;    /* 0 -> MGX_LIVELOCK_WORDS */
+    int32_t terminal_mode;     /* mgx_terminal_mode */
+    int32_t mission_int64;     /* 1: mission tokens int64 (TokenizeVocabWrapper dtype), 0: uint8 */
+    int32_t reserved;
+    int64_t mt_table_words;    /* 0 -> default (2^24); shared MT19937 output table length */
+} mgx_config;
+
+/* Stacked observation in the layout SB3's VecFrameStack(VecTransposeImage(.))
+ * hands the policy: image u8 [N][3*n_stack][7][7] ([c][vx][vy] per frame,
+ * newest frame last), direction u8 [N][4*n_stack] (one-hot per frame),
+ * mission [N][32*n_stack] (int64 or uint8 tokens per frame). */
+typedef struct mgx_obs {
+    void *image_dev;
+    void *direction_dev;
+    void *mission_dev;
+} mgx_obs;
+
+typedef struct mgx_step_out {
+    mgx_obs obs;               /* updated in place (the stacks roll) */
+    mgx_obs terminal;          /* stacked terminal obs, valid where written (terminal_mode) */
+    float *reward_dev;         /* f32 [N] */
+    double *reward64_dev;      /* f64 [N] (optional): the env's Python-float reward */
+    uint8_t *terminated_dev;   /* u8 [N] */
+    uint8_t *truncated_dev;    /* u8 [N] (gymnasium truncated; TimeLimit.truncated = trunc & !term) */
+    uint8_t *done_dev;         /* u8 [N] = term | trunc (SB3 `dones`) */
+    float *ep_return_dev;      /* f32 [N] Monitor 'r', valid where done (optional) */
+    int32_t *ep_len_dev;       /* i32 [N] Monitor 'l', valid where done (optional) */
+    int32_t *livelock_dev;     /* i32 [N] abandoned reset attempts where done (optional) */
+} mgx_step_out;
+
+typedef struct mgx_handle mgx_handle;
+
+const char *mgx_last_error(void);
+int mgx_abi_version(void);
+
+mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out);
+mgx_status mgx_destroy(mgx_handle *h);
+
+/* First (seeded) reset of every env; writes the stacked first observation
+ * (zeros + newest frame).  `livelock_dev` (optional i32 [N]). */
+mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, void *stream);
+
+/* One vectorised step.  actions_dev: [N] int32 (action_bytes = 4) or int64 (8). */
+mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes,
+                    const mgx_step_out *out, void *stream);
+
+/* GAE over a [T][N] f32 rollout (DictRolloutBuffer.compute_returns_and_advantage):
+ * episode_starts_dev f32 [T][N], last_values f32 [N], last_dones u8 [N];
+ * writes advantages/returns f32 [T][N].  adv_stats_dev (optional, f64 [3]):
+ * accumulates (sum A, sum A^2, count) for RCCL advantage-stat reduction. */
+mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const float *episode_starts_dev,
+                   const float *last_values_dev, const uint8_t *last_dones_dev, int64_t T, int64_t N,
+                   float gamma, float gamma_lambda, float *advantages_dev, float *returns_dev,
+                   double *adv_stats_dev, void *stream);
+
+/* Synchronises `stream`, returns the device error bits (MGX_DEVERR_*) and clears them. */
+mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits);
+
+/* Counters since create: [0] env-steps, [1] resets (incl. first), [2] abandoned
+ * (live-locked) reset attempts, [3] max MT cursor.  Synchronises `stream`. */
+mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[4]);
+
+/* Test/debug: copy env state to HOST buffers (any may be NULL); synchronises.
+ * grid u8 [N][S][S][4] (x-major (type,colour,state,box-holds-key)), agent u8 [N][3],
+ * carrying u8 [N][4], step_count i32 [N], mission_done u8 [N], stored_reward f64 [N]
+ * (NaN = None), mt_words i64 [N], pcg u64 [N][6] (state hi/lo, inc hi/lo,
+ * has_uint32, uinteger), target u8 [N][3], mission_id u8 [N]. */
+mgx_status mgx_dump_state(mgx_handle *h, void *stream, uint8_t *grid, uint8_t *agent, uint8_t *carrying,
+                          int32_t *step_count, uint8_t *mission_done, double *stored_reward,
+                          int64_t *mt_words, uint64_t *pcg, uint8_t *target, uint8_t *mission_id);
+
+/* Mission text / tokens for a mission_id (host side, no device access). */
+mgx_status mgx_mission_text(int mission_id, char *buf, size_t buflen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGX_H_ */

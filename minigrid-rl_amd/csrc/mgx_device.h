@@ -1,0 +1,694 @@
+// mgx_device.h -- device-side MiniGrid semantics for the MI355X engine.
+//
+// One env per lane.  Env grids are 1 byte per cell (code below), staged per
+// workgroup in LDS; reset generation runs on the env's LDS grid slot with the
+// shared MT19937 output table read through a per-lane LDS window.
+//
+// Reference behaviour reproduced (file:line into /root/reference):
+//   PlaygroundEnv.step             src/custom_env.py:269-330   -> step_env()
+//   PlaygroundEnv._gen_grid        src/custom_env.py:122-267   -> gen_attempt()/reset_env()
+//   _generate_multi_map            src/custom_env.py:595-615   -> gen_multi()
+//   _generate_2/3/4_rooms          src/custom_env.py:617-2034  -> gen_2/3/4_rooms()
+//   _generate_{gto,gtg,open,pkp}   src/custom_env.py:371-513   -> gen_single()
+//   next2door                      src/custom_env.py:2036-2046 -> next2door()
+//   TokenizeVocabWrapper           src/environment.py:91-112   -> host mission table
+//   Discrete2BoxWrapper            src/environment.py:144-149  -> one-hot direction stack
+// plus minigrid's MiniGridEnv.step/gen_obs/place_obj/place_agent (3P),
+// CPython random (_randbelow via getrandbits) and numpy PCG64/Generator.integers (A.6).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mgx {
+
+// ---------------------------------------------------------------- cell code
+// bits 0-3: OBJECT_TO_IDX type (1 empty, 2 wall, 4 door closed/locked, 5 key,
+// 6 ball, 7 box, 8 goal, 9 lava, 11 = OPEN door); bits 4-6: COLOR_TO_IDX;
+// bit 7: aux (door: locked; box: holds a Key of its colour).  0 = "nothing"
+// (only used for the carried-object slot).
+constexpr uint8_t CODE_EMPTY = 0x01;
+constexpr uint8_t CODE_WALL = 2 | (5 << 4);   // Wall() is grey
+constexpr uint8_t CODE_GOAL = 8 | (1 << 4);   // Goal() is green
+constexpr int T_EMPTY = 1, T_WALL = 2, T_DOOR = 4, T_KEY = 5, T_BALL = 6, T_BOX = 7,
+              T_GOAL = 8, T_LAVA = 9, T_OPEN = 11;
+constexpr int A_LEFT = 0, A_RIGHT = 1, A_FORWARD = 2, A_PICKUP = 3, A_DROP = 4,
+              A_TOGGLE = 5, A_DONE = 6;
+constexpr uint8_t NONE8 = 0xFF;
+
+// COLOR_NAMES (sorted) index -> COLOR_TO_IDX
+__device__ __forceinline__ int cn2idx(int cn) { return (0x403512 >> (cn * 4)) & 0xF; }  // {2,1,5,3,0,4}
+
+__device__ __forceinline__ uint8_t mk_code(int t, int cidx, int aux) {
+    return (uint8_t)(t | (cidx << 4) | (aux << 7));
+}
+__device__ __forceinline__ bool is_door(uint8_t c) { int t = c & 15; return t == T_DOOR || t == T_OPEN; }
+__device__ __forceinline__ bool can_overlap(uint8_t c) {
+    int t = c & 15; return t == T_EMPTY || t == T_GOAL || t == T_LAVA || t == T_OPEN;
+}
+__device__ __forceinline__ bool can_pickup(uint8_t c) { int t = c & 15; return t >= T_KEY && t <= T_BOX; }
+
+// WorldObj.encode(): returns type | colour<<8 | state<<16
+__device__ __forceinline__ uint32_t encode3(uint8_t code) {
+    uint32_t t = code & 15, c = (code >> 4) & 7, a = code >> 7;
+    uint32_t s = (t == T_DOOR) ? 1u + a : 0u;
+    t = (t == T_OPEN) ? (uint32_t)T_DOOR : t;
+    return t | (c << 8) | (s << 16);
+}
+
+// ------------------------------------------------------------ env state
+struct __align__(16) EnvState {
+    uint8_t ax, ay, dir, carry;      // carry: cell code, 0 = None
+    uint16_t step_count;
+    int16_t reward_step;             // step_count at mission completion (self.reward), -1 = None
+    uint8_t tx, ty;                  // target_pos, NONE8 = None
+    uint8_t target_action;           // NONE8 = None
+    uint8_t mission_id;              // cmd | colour-name<<2 | type-slot<<5 (host table)
+    uint8_t mission_done;
+    uint8_t frames;                  // frames of the current episode in the stack (<= n_stack)
+    uint8_t flags;
+    uint8_t pad;
+};
+static_assert(sizeof(EnvState) == 16, "EnvState must be 16 bytes");
+
+// mission ids
+constexpr int CMD_GOTO = 0, CMD_TOGGLE = 1, CMD_PICKUP = 2, CMD_GOTOGOAL = 3;
+constexpr int TS_DOOR = 0, TS_KEY = 1, TS_BALL = 2, TS_BOX = 3;
+__device__ __forceinline__ int type_slot(int t) {
+    return t == T_DOOR ? TS_DOOR : t == T_KEY ? TS_KEY : t == T_BALL ? TS_BALL : TS_BOX;
+}
+
+__device__ __forceinline__ double reward_at(int sc, int max_steps) {
+    // MiniGridEnv._reward: 1 - 0.9 * (step_count / max_steps), fp64, no contraction
+    double q = (double)sc / (double)max_steps;
+    double m = __dmul_rn(0.9, q);
+    return __dsub_rn(1.0, m);
+}
+
+// ------------------------------------------------------------ render
+// gen_obs(): 7x7 egocentric view, [c][vx][vy] frame (VecTransposeImage layout).
+// View cell (vx,vy) = world A + (6-vy)*dir_vec + (vx-3)*right_vec (== minigrid's
+// slice + (dir+1) x rotate_left); out of bounds -> Wall; (3,6) -> carried or None.
+template <typename Store>
+__device__ __forceinline__ void render_view(const uint8_t *g, int S, int ax, int ay, int dir,
+                                            uint8_t carry, Store store) {
+    const int dx = (dir == 0) - (dir == 2);
+    const int dy = (dir == 1) - (dir == 3);
+    const int rx = -dy, ry = dx;
+#pragma unroll
+    for (int vx = 0; vx < 7; ++vx) {
+#pragma unroll
+        for (int vy = 0; vy < 7; ++vy) {
+            uint8_t code;
+            if (vx == 3 && vy == 6) {
+                code = carry ? carry : CODE_EMPTY;
+            } else {
+                int wx = ax + (6 - vy) * dx + (vx - 3) * rx;
+                int wy = ay + (6 - vy) * dy + (vx - 3) * ry;
+                bool in = (unsigned)wx < (unsigned)S && (unsigned)wy < (unsigned)S;
+                code = in ? g[wy * S + wx] : CODE_WALL;
+            }
+            uint32_t e = encode3(code);
+            store(vx * 7 + vy, e);
+        }
+    }
+}
+
+// ------------------------------------------------------------ PCG64 / SeedSequence
+constexpr uint64_t PCG_MH = 2549297995355413924ULL, PCG_ML = 4865540595714422341ULL;
+
+struct Pcg {
+    uint64_t sh, sl, ih, il;
+    uint32_t has, uinteger;
+};
+
+__device__ __forceinline__ void pcg_step(Pcg &p) {
+    uint64_t lo = p.sl * PCG_ML;
+    uint64_t hi = __umul64hi(p.sl, PCG_ML) + p.sl * PCG_MH + p.sh * PCG_ML;
+    uint64_t nlo = lo + p.il;
+    hi += p.ih + (nlo < lo ? 1ull : 0ull);
+    p.sh = hi;
+    p.sl = nlo;
+}
+__device__ __forceinline__ uint64_t pcg_next64(Pcg &p) {
+    pcg_step(p);
+    uint32_t rot = (uint32_t)(p.sh >> 58);
+    uint64_t x = p.sh ^ p.sl;
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+__device__ __forceinline__ uint32_t pcg_next32(Pcg &p) {
+    if (p.has) { p.has = 0; return p.uinteger; }
+    uint64_t n = pcg_next64(p);
+    p.has = 1;
+    p.uinteger = (uint32_t)(n >> 32);
+    return (uint32_t)n;
+}
+// Generator.integers(lo, hi) (exclusive hi), scalar path: buffered Lemire32.
+__device__ __forceinline__ int pcg_integers(Pcg &p, int lo, int hi) {
+    uint32_t rng = (uint32_t)(hi - 1 - lo);
+    if (rng == 0) return lo;
+    uint32_t rng_excl = rng + 1u;
+    uint64_t m = (uint64_t)pcg_next32(p) * rng_excl;
+    uint32_t left = (uint32_t)m;
+    if (left < rng_excl) {
+        uint32_t thr = (0xffffffffu - rng) % rng_excl;
+        while (left < thr) {
+            m = (uint64_t)pcg_next32(p) * rng_excl;
+            left = (uint32_t)m;
+        }
+    }
+    return lo + (int)(m >> 32);
+}
+
+// numpy SeedSequence(seed).generate_state(4, uint64) -> PCG64 seeding.
+__device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t &hc) {
+    v ^= hc; hc *= 0x931e8875u; v *= hc; v ^= v >> 16; return v;
+}
+__device__ __forceinline__ uint32_t ss_mix(uint32_t x, uint32_t y) {
+    uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y; r ^= r >> 16; return r;
+}
+__device__ inline void pcg_seed(Pcg &p, uint64_t seed) {
+    uint32_t e0 = (uint32_t)seed, e1 = (uint32_t)(seed >> 32);
+    int nent = (seed >> 32) ? 2 : 1;
+    uint32_t pool[4];
+    uint32_t hc = 0x43b0d7e5u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) pool[i] = ss_hashmix(i == 0 ? e0 : (i == 1 && nent == 2 ? e1 : 0u), hc);
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+            if (s != d) pool[d] = ss_mix(pool[d], ss_hashmix(pool[s], hc));
+    uint32_t w[8];
+    uint32_t hb = 0x8b51f9ddu;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint32_t v = pool[i & 3];
+        v ^= hb; hb *= 0x58f38dedu; v *= hb; v ^= v >> 16;
+        w[i] = v;
+    }
+    uint64_t v0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32), v1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+    uint64_t v2 = (uint64_t)w[4] | ((uint64_t)w[5] << 32), v3 = (uint64_t)w[6] | ((uint64_t)w[7] << 32);
+    // initstate = v0:v1, initseq = v2:v3; inc = initseq<<1 | 1
+    p.ih = (v2 << 1) | (v3 >> 63);
+    p.il = (v3 << 1) | 1ull;
+    p.sh = 0; p.sl = 0;
+    pcg_step(p);
+    uint64_t nl = p.sl + v1;
+    p.sh = p.sh + v0 + (nl < p.sl ? 1ull : 0ull);
+    p.sl = nl;
+    pcg_step(p);
+    p.has = 0; p.uinteger = 0;
+}
+
+// ------------------------------------------------------------ generator context
+constexpr int MT_WIN = 64;        // words per lane-private LDS window
+constexpr int WIN_STRIDE = 68;    // words; 68 mod 32 = 4 -> b128 writes spread over banks
+constexpr int MAX_OBJS = 32;
+constexpr int SAT_PROBE = 64;     // rejections before the exhaustive satisfiability probe
+constexpr uint32_t PCG_LOOP_LIMIT = 1u << 20;
+
+struct Gen {
+    uint8_t *g;            // LDS grid slot (S*S used, row-major y*S+x)
+    int S;
+    // MT19937 shared table + cursor
+    const uint32_t *table;
+    uint64_t tlen;
+    uint32_t *win;         // LDS window (MT_WIN words, 16-B aligned)
+    uint64_t wbase, cur, astart;
+    uint32_t llw;
+    bool abort;
+    uint32_t err;
+    Pcg pcg;
+    int ax, ay, adir;
+    uint32_t *objs;        // LDS objs list: type | cname<<4 | x<<8 | y<<16 (cname 15 = None)
+    int nobjs;
+    // config
+    int problem, cfg_mission, num_objects, all_doors_open;
+};
+
+__device__ __forceinline__ uint8_t &cell(Gen &G, int x, int y) { return G.g[y * G.S + x]; }
+
+// Refill the lane's LDS window with table[cur & ~3 .. +MT_WIN) (16 independent
+// 16-B loads in flight, one HBM/L2 round trip per window).
+__device__ __forceinline__ uint64_t mt_refill(const uint32_t *__restrict__ table, uint64_t tlen, uint32_t *win,
+                                              uint64_t cur, uint32_t &err) {
+    uint64_t base = cur & ~3ull;
+    if (base + MT_WIN > tlen) { err |= 1u; base = tlen; }   // MGX_DEVERR_MT_TABLE: read the zero pad
+    const uint4 *src = reinterpret_cast<const uint4 *>(table + base);
+    uint4 *dst = reinterpret_cast<uint4 *>(win);
+#pragma unroll
+    for (int k = 0; k < MT_WIN / 4; k++) dst[k] = src[k];
+    return base;
+}
+
+__device__ __forceinline__ uint32_t mt_word(Gen &G) {
+    if (G.cur - G.astart >= G.llw) { G.abort = true; return 0; }
+    uint64_t off = G.cur - G.wbase;
+    if (off >= MT_WIN) {
+        G.wbase = mt_refill(G.table, G.tlen, G.win, G.cur, G.err);
+        off = G.cur - G.wbase;
+        if (off >= MT_WIN) off = 0;   // only after MGX_DEVERR_MT_TABLE
+    }
+    G.cur++;
+    return G.win[off];
+}
+// random._randbelow_with_getrandbits(n), n >= 1
+__device__ __forceinline__ int randbelow(Gen &G, uint32_t n) {
+    int k = 32 - __clz(n);
+    for (;;) {
+        uint32_t w = mt_word(G);
+        if (G.abort) return 0;
+        uint32_t r = k == 32 ? w : (w >> (32 - k));
+        if (r < n) return (int)r;
+    }
+}
+__device__ __forceinline__ int randint(Gen &G, int a, int b) { return a + randbelow(G, (uint32_t)(b - a + 1)); }
+__device__ __forceinline__ bool choice_bool(Gen &G) { return randbelow(G, 2) == 0; }   // choice([True, False])
+
+__device__ __forceinline__ bool next2door(Gen &G, int x, int y) {
+    return is_door(cell(G, x - 1, y)) || is_door(cell(G, x + 1, y)) ||
+           is_door(cell(G, x, y - 1)) || is_door(cell(G, x, y + 1));
+}
+
+__device__ __forceinline__ void add_obj(Gen &G, int t, int cname, int x, int y) {
+    if (G.nobjs >= MAX_OBJS) { G.err |= 8u; return; }
+    G.objs[G.nobjs++] = (uint32_t)t | ((uint32_t)(cname & 15) << 4) | ((uint32_t)x << 8) | ((uint32_t)y << 16);
+}
+
+// MiniGridEnv.place_obj(obj) over the whole grid (PCG64)
+__device__ inline void place_obj_any(Gen &G, uint8_t code, int &px, int &py) {
+    for (uint32_t it = 0;; ++it) {
+        if (it > PCG_LOOP_LIMIT) { G.err |= 4u; px = 1; py = 1; return; }
+        int x = pcg_integers(G.pcg, 0, G.S);
+        int y = pcg_integers(G.pcg, 0, G.S);
+        if (cell(G, x, y) != CODE_EMPTY) continue;
+        if (x == G.ax && y == G.ay) continue;
+        cell(G, x, y) = code;
+        px = x; py = y;
+        return;
+    }
+}
+__device__ inline void place_agent(Gen &G) {
+    G.ax = -1; G.ay = -1;
+    int x, y;
+    place_obj_any(G, CODE_EMPTY, x, y);
+    G.ax = x; G.ay = y;
+    G.adir = pcg_integers(G.pcg, 0, 4);
+}
+
+// ---- ordered choice lists as bitmasks (list.remove keeps order) --------------
+// element b of an obj_choice list = (types[b / 6], COLOR_NAMES[b % 6])
+__device__ __forceinline__ int nth_set_bit(uint32_t m, int r) {
+    for (int i = 0; i < r; i++) m &= m - 1;
+    return __ffs(m) - 1;
+}
+__device__ __forceinline__ int mask_choice(Gen &G, uint32_t m) {   // index into the list
+    return nth_set_bit(m, randbelow(G, (uint32_t)__popc(m)));
+}
+
+__device__ __forceinline__ void live_lock(Gen &G) {
+    // provably unsatisfiable `while True` loop: the reference would spin until the
+    // cap; that consumes exactly llw words of this attempt -- jump there.
+    G.cur = G.astart + G.llw;
+    G.abort = true;
+}
+
+// `while True: p=(randint(x0,x1), randint(y0,y1)); if p!=goal and [p!=agent] and
+//  [p!=other] and not next2door(p): break` -> grid.set(Box(c,Key(c)) | Key(c)); objs.append
+__device__ inline void place_key(Gen &G, int x0, int x1, int y0, int y1, int gx, int gy, bool chk_agent,
+                                 int ox, int oy, int cname, bool kib, int *kx, int *ky) {
+    int x, y, rej = 0;
+    for (;;) {
+        x = randint(G, x0, x1);
+        y = randint(G, y0, y1);
+        if (G.abort) return;
+        bool bad = (x == gx && y == gy) || (chk_agent && x == G.ax && y == G.ay) || (x == ox && y == oy) ||
+                   next2door(G, x, y);
+        if (!bad) break;
+        if (++rej == SAT_PROBE) {
+            bool sat = false;
+            for (int xx = x0; xx <= x1 && !sat; xx++)
+                for (int yy = y0; yy <= y1 && !sat; yy++)
+                    sat = !((xx == gx && yy == gy) || (chk_agent && xx == G.ax && yy == G.ay) ||
+                            (xx == ox && yy == oy) || next2door(G, xx, yy));
+            if (!sat) { live_lock(G); return; }
+        }
+    }
+    int cidx = cn2idx(cname);
+    if (kib) { cell(G, x, y) = mk_code(T_BOX, cidx, 1); add_obj(G, T_BOX, cname, x, y); }
+    else { cell(G, x, y) = mk_code(T_KEY, cidx, 0); add_obj(G, T_KEY, cname, x, y); }
+    if (kx) { *kx = x; *ky = y; }
+}
+
+// `for _ in range(n): (t,c)=choice(obj_choice); obj_choice.remove((t,c)); while True:
+//  p=(randint..); [p in objs -> retry]; if p != agent and not next2door(p): break; put_obj`
+// (p in objs <=> grid cell occupied, inside a room interior)
+__device__ inline void place_objects(Gen &G, uint32_t &oc, const int *types, int n, int x0, int x1,
+                                     int y0, int y1) {
+    for (int k = 0; k < n; k++) {
+        if (oc == 0) { G.err |= 8u; return; }
+        int b = mask_choice(G, oc);
+        if (G.abort) return;
+        oc &= ~(1u << b);
+        int t = types[b / 6], cname = b % 6;
+        int x, y, rej = 0;
+        for (;;) {
+            x = randint(G, x0, x1);
+            y = randint(G, y0, y1);
+            if (G.abort) return;
+            bool bad = cell(G, x, y) != CODE_EMPTY || (x == G.ax && y == G.ay) || next2door(G, x, y);
+            if (!bad) break;
+            if (++rej == SAT_PROBE) {
+                bool sat = false;
+                for (int xx = x0; xx <= x1 && !sat; xx++)
+                    for (int yy = y0; yy <= y1 && !sat; yy++)
+                        sat = !(cell(G, xx, yy) != CODE_EMPTY || (xx == G.ax && yy == G.ay) || next2door(G, xx, yy));
+                if (!sat) { live_lock(G); return; }
+            }
+        }
+        cell(G, x, y) = mk_code(t, cn2idx(cname), 0);
+        add_obj(G, t, cname, x, y);
+    }
+}
+
+__device__ inline void place_goal_multi(Gen &G, int &gx, int &gy) {
+    for (uint32_t it = 0;; ++it) {
+        if (it > PCG_LOOP_LIMIT) { G.err |= 4u; break; }
+        place_obj_any(G, CODE_GOAL, gx, gy);
+        if (next2door(G, gx, gy)) { cell(G, gx, gy) = CODE_EMPTY; continue; }
+        break;
+    }
+    add_obj(G, T_GOAL, 15, gx, gy);
+}
+
+__device__ __forceinline__ int door_code(int cname, bool locked, bool open) {
+    return open ? mk_code(T_OPEN, cn2idx(cname), 0) : mk_code(T_DOOR, cn2idx(cname), locked ? 1 : 0);
+}
+
+// obj_choice removal when a door is locked: bits ('key', c) = c, ('box', c) = 12 + c
+struct DoorDraw { int col; bool lk, kib; };
+__device__ inline DoorDraw draw_door(Gen &G, uint32_t &dcols, uint32_t &oc) {
+    DoorDraw d;
+    d.col = mask_choice(G, dcols);
+    dcols &= ~(1u << d.col);
+    d.lk = G.all_doors_open ? false : choice_bool(G);
+    d.kib = choice_bool(G);
+    if (d.lk) { oc &= ~(1u << d.col); if (d.kib) oc &= ~(1u << (12 + d.col)); }
+    return d;
+}
+__device__ inline void set_door(Gen &G, const DoorDraw &d, int x, int y) {
+    bool open = G.all_doors_open ? choice_bool(G) : false;
+    cell(G, x, y) = (uint8_t)door_code(d.col, d.lk, open);
+    add_obj(G, T_DOOR, d.col, x, y);
+}
+
+__device__ const int MULTI_TYPES[3] = {T_KEY, T_BALL, T_BOX};
+
+__device__ inline void gen_2_rooms(Gen &G, int mid) {          // custom_env.py:617-855
+    const int S = G.S;
+    int n_left = G.num_objects / 2, n_right = G.num_objects - n_left;
+    uint32_t oc = 0x3FFFFu;
+    for (int i = 1; i < S - 1; i++) cell(G, mid, i) = CODE_WALL;
+    uint32_t dc = 0x3Fu;
+    DoorDraw d = draw_door(G, dc, oc);
+    if (G.abort) return;
+    int j = randint(G, 1, S - 2);
+    set_door(G, d, mid, j);
+    if (G.abort) return;
+    int gx, gy;
+    place_goal_multi(G, gx, gy);
+    bool goal_left = gx < mid;
+    place_agent(G);
+    bool a_left = G.ax < mid;
+    if (a_left && d.lk) { n_left--; place_key(G, 1, mid - 1, 1, S - 2, gx, gy, true, -1, -1, d.col, d.kib, 0, 0); }
+    if (G.abort) return;
+    if (goal_left) n_left--;
+    place_objects(G, oc, MULTI_TYPES, n_left, 1, mid - 1, 1, S - 2);
+    if (G.abort) return;
+    if (!a_left && d.lk) { n_right--; place_key(G, mid + 1, S - 2, 1, S - 2, gx, gy, true, -1, -1, d.col, d.kib, 0, 0); }
+    if (G.abort) return;
+    if (!goal_left) n_right--;
+    place_objects(G, oc, MULTI_TYPES, n_right, mid + 1, S - 2, 1, S - 2);
+}
+
+__device__ inline void gen_3_rooms(Gen &G, int mid) {          // custom_env.py:857-1297
+    const int S = G.S;
+    int n_left = G.num_objects / 2;
+    int n_lu = n_left / 2, n_right = G.num_objects - n_left;
+    uint32_t oc = 0x3FFFFu;
+    for (int i = 1; i < S - 1; i++) cell(G, mid, i) = CODE_WALL;
+    for (int i = 1; i < mid; i++) cell(G, i, mid) = CODE_WALL;
+    uint32_t dc = 0x3Fu;
+    DoorDraw h = draw_door(G, dc, oc);
+    DoorDraw vu = draw_door(G, dc, oc);
+    DoorDraw vl = draw_door(G, dc, oc);
+    if (G.abort) return;
+    int h_i = randint(G, 1, mid - 1); set_door(G, h, h_i, mid);
+    int vu_j = randint(G, 1, mid - 1); set_door(G, vu, mid, vu_j);
+    int vl_j = randint(G, mid + 1, S - 2); set_door(G, vl, mid, vl_j);
+    if (G.abort) return;
+    int gx, gy;
+    place_goal_multi(G, gx, gy);
+    bool g_left = gx < mid, g_up = gy < mid;
+    place_agent(G);
+    bool a_left = G.ax < mid, a_up = G.ay < mid;
+    if (a_left && a_up) {      // upper left
+        int kx = -1, ky = -1;
+        if (vu.lk) { n_lu--; place_key(G, 1, mid - 1, 1, mid - 1, gx, gy, true, -1, -1, vu.col, vu.kib, &kx, &ky); }
+        if (G.abort) return;
+        if (h.lk) { n_lu--; place_key(G, 1, mid - 1, 1, mid - 1, gx, gy, true, kx, ky, h.col, h.kib, 0, 0); }
+        if (G.abort) return;
+    }
+    if (g_left && g_up) n_lu--;
+    place_objects(G, oc, MULTI_TYPES, n_lu, 1, mid - 1, 1, mid - 1);
+    if (G.abort) return;
+    if (a_left && !a_up) {     // lower left
+        int kx = -1, ky = -1;
+        if (vl.lk) { place_key(G, 1, mid - 1, mid + 1, S - 2, gx, gy, true, -1, -1, vl.col, vl.kib, &kx, &ky); }
+        if (G.abort) return;
+        if (h.lk) { place_key(G, 1, mid - 1, mid + 1, S - 2, gx, gy, true, kx, ky, h.col, h.kib, 0, 0); }
+        if (G.abort) return;
+    }
+    // Q1 (custom_env.py:1119): the lower-left loop runs num_left_upper_objects times
+    place_objects(G, oc, MULTI_TYPES, n_lu, 1, mid - 1, mid + 1, S - 2);
+    if (G.abort) return;
+    if (!a_left) {             // right
+        int kx = -1, ky = -1;
+        if (vl.lk) { n_right--; place_key(G, mid + 1, S - 2, 1, S - 2, gx, gy, true, -1, -1, vl.col, vl.kib, &kx, &ky); }
+        if (G.abort) return;
+        if (vu.lk) { n_right--; place_key(G, mid + 1, S - 2, 1, S - 2, gx, gy, true, kx, ky, vu.col, vu.kib, 0, 0); }
+        if (G.abort) return;
+    }
+    if (!g_left) n_right--;
+    place_objects(G, oc, MULTI_TYPES, n_right, mid + 1, S - 2, 1, S - 2);
+}
+
+__device__ inline void gen_4_rooms(Gen &G, int mid) {          // custom_env.py:1299-2034
+    const int S = G.S;
+    int n_left = G.num_objects / 2;
+    int n_lu = n_left / 2;
+    int n_right = G.num_objects - n_left;
+    int n_ru = n_right / 2, n_rl = n_right - n_ru;
+    uint32_t oc = 0x3FFFFu;
+    for (int i = 1; i < S - 1; i++) cell(G, mid, i) = CODE_WALL;
+    for (int i = 1; i < S - 1; i++) cell(G, i, mid) = CODE_WALL;
+    uint32_t dc = 0x3Fu;
+    DoorDraw hl = draw_door(G, dc, oc);
+    DoorDraw hr = draw_door(G, dc, oc);
+    DoorDraw vu = draw_door(G, dc, oc);
+    DoorDraw vl = draw_door(G, dc, oc);
+    if (G.abort) return;
+    int hl_i = randint(G, 1, mid - 1); set_door(G, hl, hl_i, mid);
+    int hr_i = randint(G, mid + 1, S - 2); set_door(G, hr, hr_i, mid);
+    int vu_j = randint(G, 1, mid - 1); set_door(G, vu, mid, vu_j);
+    int vl_j = randint(G, mid + 1, S - 2); set_door(G, vl, mid, vl_j);
+    if (G.abort) return;
+    int gx, gy;
+    place_goal_multi(G, gx, gy);
+    bool g_left = gx < mid, g_up = gy < mid;
+    place_agent(G);
+    bool a_left = G.ax < mid, a_up = G.ay < mid;
+    const int L0 = 1, L1 = mid - 1, R0 = mid + 1, R1 = S - 2;
+    // upper left (custom_env.py:1414-1530)
+    if (a_left && a_up) {
+        int kx = -1, ky = -1;
+        if (vu.lk) { n_lu--; place_key(G, L0, L1, L0, L1, gx, gy, true, -1, -1, vu.col, vu.kib, &kx, &ky); }
+        if (G.abort) return;
+        if (hl.lk) { n_lu--; place_key(G, L0, L1, L0, L1, gx, gy, true, kx, ky, hl.col, hl.kib, 0, 0); }
+    } else if (a_left && !a_up) {
+        if (vu.lk) { n_lu--; place_key(G, L0, L1, L0, L1, gx, gy, false, -1, -1, vu.col, vu.kib, 0, 0); }
+    } else if (!a_left && a_up) {
+        if (hl.lk) { n_lu--; place_key(G, L0, L1, L0, L1, gx, gy, false, -1, -1, hl.col, hl.kib, 0, 0); }
+    }
+    if (G.abort) return;
+    if (g_left && g_up) n_lu--;
+    place_objects(G, oc, MULTI_TYPES, n_lu, L0, L1, L0, L1);
+    if (G.abort) return;
+    // lower left (custom_env.py:1569-1685)
+    if (a_left && !a_up) {
+        int kx = -1, ky = -1;
+        if (vl.lk) { place_key(G, L0, L1, R0, R1, gx, gy, true, -1, -1, vl.col, vl.kib, &kx, &ky); }
+        if (G.abort) return;
+        if (hl.lk) { place_key(G, L0, L1, R0, R1, gx, gy, true, kx, ky, hl.col, hl.kib, 0, 0); }
+    } else if (!a_left && !a_up) {
+        if (hl.lk) { place_key(G, L0, L1, R0, R1, gx, gy, false, -1, -1, hl.col, hl.kib, 0, 0); }
+    } else if (a_left && a_up) {
+        if (vl.lk) { place_key(G, L0, L1, R0, R1, gx, gy, false, -1, -1, vl.col, vl.kib, 0, 0); }
+    }
+    if (G.abort) return;
+    // Q1 (custom_env.py:1660): the lower-left loop runs num_left_upper_objects times
+    place_objects(G, oc, MULTI_TYPES, n_lu, L0, L1, R0, R1);
+    if (G.abort) return;
+    // upper right (custom_env.py:1724-1841)
+    if (!a_left && a_up) {
+        int kx = -1, ky = -1;
+        if (vu.lk) { n_ru--; place_key(G, R0, R1, L0, L1, gx, gy, true, -1, -1, vu.col, vu.kib, &kx, &ky); }
+        if (G.abort) return;
+        if (hr.lk) { n_ru--; place_key(G, R0, R1, L0, L1, gx, gy, true, kx, ky, hr.col, hr.kib, 0, 0); }
+    } else if (!a_left && !a_up) {
+        if (vu.lk) { n_ru--; place_key(G, R0, R1, L0, L1, gx, gy, false, -1, -1, vu.col, vu.kib, 0, 0); }
+    } else if (a_left && a_up) {
+        if (hr.lk) { n_ru--; place_key(G, R0, R1, L0, L1, gx, gy, false, -1, -1, hr.col, hr.kib, 0, 0); }
+    }
+    if (G.abort) return;
+    if (!g_left && g_up) n_ru--;
+    place_objects(G, oc, MULTI_TYPES, n_ru, R0, R1, L0, L1);
+    if (G.abort) return;
+    // lower right (custom_env.py:1880-1997)
+    if (!a_left && !a_up) {
+        int kx = -1, ky = -1;
+        if (vl.lk) { n_rl--; place_key(G, R0, R1, R0, R1, gx, gy, true, -1, -1, vl.col, vl.kib, &kx, &ky); }
+        if (G.abort) return;
+        if (hr.lk) { n_rl--; place_key(G, R0, R1, R0, R1, gx, gy, true, kx, ky, hr.col, hr.kib, 0, 0); }
+    } else if (a_left && !a_up) {
+        if (hr.lk) { n_rl--; place_key(G, R0, R1, R0, R1, gx, gy, false, -1, -1, hr.col, hr.kib, 0, 0); }
+    } else if (!a_left && a_up) {
+        if (vl.lk) { n_rl--; place_key(G, R0, R1, R0, R1, gx, gy, false, -1, -1, vl.col, vl.kib, 0, 0); }
+    }
+    if (G.abort) return;
+    if (!g_left && !g_up) n_rl--;
+    place_objects(G, oc, MULTI_TYPES, n_rl, R0, R1, R0, R1);
+}
+
+__device__ inline int gen_multi(Gen &G) {                      // custom_env.py:595-615
+    int cmd;
+    if (G.cfg_mission >= 0) cmd = G.cfg_mission;
+    else {
+        int r = randbelow(G, 4);                                 // choice([0, 1, 2, 5])
+        cmd = r == 3 ? 5 : r;
+    }
+    if (G.abort) return 0;
+    int mid = G.S / 2;
+    int nr = randint(G, 2, 4);
+    if (G.abort) return 0;
+    if (nr == 2) gen_2_rooms(G, mid);
+    else if (nr == 3) gen_3_rooms(G, mid);
+    else gen_4_rooms(G, mid);
+    return cmd;
+}
+
+__device__ const int GTO_T[4] = {T_KEY, T_BALL, T_BOX, T_DOOR};   // self.obj_types
+__device__ const int GTG_T[4] = {T_BOX, T_DOOR, T_KEY, T_BALL};
+__device__ const int OPN_T[2] = {T_BOX, T_DOOR};
+__device__ const int PKP_T[3] = {T_KEY, T_BOX, T_BALL};
+
+__device__ inline int gen_single(Gen &G) {                     // custom_env.py:371-513
+    const int *types;
+    int ntypes, cmd;
+    bool goal = false;
+    switch (G.problem) {
+        case 2: types = GTO_T; ntypes = 4; cmd = 0; break;             // gto -> 'go to'
+        case 3: types = GTG_T; ntypes = 4; cmd = 5; goal = true; break; // gtg -> 'go to goal'
+        case 4: types = OPN_T; ntypes = 2; cmd = 1; break;             // opn -> 'toggle'
+        default: types = PKP_T; ntypes = 3; cmd = 2; break;            // pkp -> 'pick up'
+    }
+    uint32_t oc = (1u << (ntypes * 6)) - 1u;
+    for (int k = 0; k < G.num_objects; k++) {
+        if (oc == 0) { G.err |= 8u; break; }
+        int b = mask_choice(G, oc);
+        if (G.abort) return 0;
+        oc &= ~(1u << b);
+        int t = types[b / 6], cname = b % 6;
+        int x, y;
+        place_obj_any(G, mk_code(t, cn2idx(cname), 0), x, y);
+        add_obj(G, t, cname, x, y);
+    }
+    if (goal) {
+        int x, y;
+        place_obj_any(G, CODE_GOAL, x, y);
+        add_obj(G, T_GOAL, 15, x, y);
+    }
+    place_agent(G);
+    return cmd;
+}
+
+struct ResetOut {
+    uint8_t tx, ty, ta, mission_id;
+    int livelocks;
+};
+
+// One attempt of MiniGridEnv.reset -> PlaygroundEnv._gen_grid (custom_env.py:122-267).
+__device__ inline void gen_attempt(Gen &G, ResetOut &R) {
+    const int S = G.S;
+    for (int i = 0; i < S * S; i++) G.g[i] = CODE_EMPTY;
+    for (int i = 0; i < S; i++) {                                 // wall_rect(0, 0, W, H)
+        cell(G, i, 0) = CODE_WALL; cell(G, i, S - 1) = CODE_WALL;
+        cell(G, 0, i) = CODE_WALL; cell(G, S - 1, i) = CODE_WALL;
+    }
+    G.ax = -1; G.ay = -1; G.adir = 0; G.nobjs = 0;
+    int cmd = G.problem == 0 ? gen_multi(G) : gen_single(G);
+    if (G.abort) return;
+    if (cmd == 0) {                                               // 'go to' (np_random.integers)
+        int i = 0;
+        for (uint32_t it = 0;; ++it) {
+            if (it > PCG_LOOP_LIMIT) { G.err |= 4u; break; }
+            i = pcg_integers(G.pcg, 0, G.nobjs);
+            if ((G.objs[i] & 15) != T_GOAL) break;
+        }
+        uint32_t o = G.objs[i];
+        R.tx = (uint8_t)(o >> 8); R.ty = (uint8_t)(o >> 16); R.ta = A_DONE;
+        R.mission_id = (uint8_t)(CMD_GOTO | (((o >> 4) & 15) << 2) | (type_slot(o & 15) << 5));
+    } else if (cmd == 1 || cmd == 2) {                            // 'toggle' / 'pick up' (random.choice)
+        int i, rej = 0;
+        for (;;) {
+            i = randbelow(G, (uint32_t)G.nobjs);
+            if (G.abort) return;
+            int t = G.objs[i] & 15;
+            if (cmd == 1 ? (t == T_BOX || t == T_DOOR) : (t == T_BOX || t == T_KEY || t == T_BALL)) break;
+            if (++rej == SAT_PROBE) {
+                bool sat = false;
+                for (int k = 0; k < G.nobjs; k++) {
+                    int tk = G.objs[k] & 15;
+                    sat |= cmd == 1 ? (tk == T_BOX || tk == T_DOOR) : (tk == T_BOX || tk == T_KEY || tk == T_BALL);
+                }
+                if (!sat) { live_lock(G); return; }
+            }
+        }
+        uint32_t o = G.objs[i];
+        R.tx = (uint8_t)(o >> 8); R.ty = (uint8_t)(o >> 16);
+        R.ta = cmd == 1 ? A_TOGGLE : A_PICKUP;
+        R.mission_id = (uint8_t)((cmd == 1 ? CMD_TOGGLE : CMD_PICKUP) | (((o >> 4) & 15) << 2) |
+                                 (type_slot(o & 15) << 5));
+    } else {                                                      // 'go to goal'
+        R.tx = R.ty = NONE8;
+        for (int k = 0; k < G.nobjs; k++)
+            if ((G.objs[k] & 15) == T_GOAL) { R.tx = (uint8_t)(G.objs[k] >> 8); R.ty = (uint8_t)(G.objs[k] >> 16); break; }
+        R.ta = NONE8;
+        R.mission_id = CMD_GOTOGOAL;
+    }
+}
+
+// MiniGridEnv.reset with the engine's live-lock retry policy.
+__device__ inline void reset_env(Gen &G, ResetOut &R) {
+    R.livelocks = 0;
+    for (;;) {
+        G.astart = G.cur;
+        G.abort = false;
+        gen_attempt(G, R);
+        if (!G.abort) break;
+        R.livelocks++;
+        if (R.livelocks > 100000) { G.err |= 4u; break; }
+    }
+}
+
+}  // namespace mgx

@@ -1,0 +1,9 @@
+"""mgx -- MI355X-native vectorised MiniGrid (PlaygroundEnv) engine.
+
+Host-side mirror of the reference's env/rollout interface (Idokorro/MiniGrid-RL
+src/custom_env.py, src/environment.py, src/ppo.py) over libmgx.so (HIP/gfx950).
+"""
+from ._lib import MgxError, mission_text  # noqa: F401
+from .engine import MgxEngine, gae  # noqa: F401
+
+__all__ = ["MgxEngine", "MgxError", "gae", "mission_text"]

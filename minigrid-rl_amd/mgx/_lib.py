@@ -1,0 +1,96 @@
+"""ctypes binding of libmgx.so (the C ABI declared in include/mgx.h).
+
+This is the reference-side binding a Python caller uses; no torch types cross
+the ABI (device pointers are plain integers).  torch MUST be imported before
+the library is loaded so that libmgx binds to the HIP runtime torch already
+loaded (both carry SONAME libamdhip64.so.7) -- one runtime per process.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (see module docstring: load order matters)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmgx.so")
+
+MGX_OK = 0
+PROBLEMS = {"multi": 0, "full": 1, "gto": 2, "gtg": 3, "opn": 4, "pkp": 5, "drp": 6, "mov": 7}
+TERMINAL = {"none": 0, "truncated": 1, "all": 2}
+DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unknown action)",
+          4: "PCG64 rejection loop bound exceeded", 8: "object list exhausted (AssertionError)"}
+
+# Every entry point include/mgx.h declares (checked by tests/test_abi.py).
+EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
+           "mgx_gae", "mgx_poll_error", "mgx_stats", "mgx_dump_state", "mgx_mission_text")
+
+
+class MgxConfig(ctypes.Structure):
+    _fields_ = [
+        ("problem", ctypes.c_int32), ("mission", ctypes.c_int32), ("size", ctypes.c_int32),
+        ("num_objects", ctypes.c_int32), ("see_through_walls", ctypes.c_int32),
+        ("all_doors_open", ctypes.c_int32), ("obstacles", ctypes.c_int32), ("n_stack", ctypes.c_int32),
+        ("n_envs", ctypes.c_int64), ("base_seed", ctypes.c_int64), ("env_index_offset", ctypes.c_int64),
+        ("livelock_words", ctypes.c_int32), ("terminal_mode", ctypes.c_int32),
+        ("mission_int64", ctypes.c_int32), ("reserved", ctypes.c_int32), ("mt_table_words", ctypes.c_int64),
+    ]
+
+
+class MgxObs(ctypes.Structure):
+    _fields_ = [("image_dev", ctypes.c_void_p), ("direction_dev", ctypes.c_void_p),
+                ("mission_dev", ctypes.c_void_p)]
+
+
+class MgxStepOut(ctypes.Structure):
+    _fields_ = [
+        ("obs", MgxObs), ("terminal", MgxObs),
+        ("reward_dev", ctypes.c_void_p), ("reward64_dev", ctypes.c_void_p),
+        ("terminated_dev", ctypes.c_void_p), ("truncated_dev", ctypes.c_void_p), ("done_dev", ctypes.c_void_p),
+        ("ep_return_dev", ctypes.c_void_p), ("ep_len_dev", ctypes.c_void_p), ("livelock_dev", ctypes.c_void_p),
+    ]
+
+
+class MgxError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libmgx.so; fails loudly when the HIP extension has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MgxError("libmgx.so not found at %s -- run `python __graft_entry__.py build` "
+                       "(the engine has no CPU fallback)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    L.mgx_last_error.restype = ctypes.c_char_p
+    L.mgx_abi_version.restype = I
+    L.mgx_create.argtypes = [ctypes.POINTER(MgxConfig), I, ctypes.POINTER(P)]
+    L.mgx_destroy.argtypes = [P]
+    L.mgx_reset.argtypes = [P, ctypes.POINTER(MgxObs), P, P]
+    L.mgx_step.argtypes = [P, P, I, ctypes.POINTER(MgxStepOut), P]
+    L.mgx_gae.argtypes = [P, P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P]
+    L.mgx_poll_error.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]
+    L.mgx_stats.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64)]
+    L.mgx_dump_state.argtypes = [P, P] + [P] * 10
+    L.mgx_mission_text.argtypes = [I, ctypes.c_char_p, ctypes.c_size_t]
+    for name in EXPORTS:
+        getattr(L, name).restype = getattr(L, name).restype or I
+    if L.mgx_abi_version() != 1:
+        raise MgxError("libmgx ABI mismatch")
+    _lib = L
+    return L
+
+
+def check(status, what=""):
+    if status != MGX_OK:
+        raise MgxError("%s failed (status %d): %s" % (what, status, load().mgx_last_error().decode()))
+
+
+def mission_text(mission_id):
+    buf = ctypes.create_string_buffer(64)
+    check(load().mgx_mission_text(int(mission_id), buf, 64), "mgx_mission_text")
+    return buf.value.decode()

@@ -1,0 +1,171 @@
+"""MgxEngine: device-resident vectorised PlaygroundEnv (torch tensors in, torch
+tensors out, no host round trip).
+
+Mirrors the reference's env construction (`make_vec_env(make_env, n_envs,
+seed, SubprocVecEnv)` + `VecTransposeImage` + `VecFrameStack(n_stack,
+'first')`, src/ppo.py:118-126) behind one object whose `step` is one kernel
+launch (libmgx `mgx_step`).  Observation tensors are updated IN PLACE every
+step (the stacks roll); clone them if you keep them across steps.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+_P = ctypes.c_void_p
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class MgxEngine:
+    def __init__(self, problem="multi", mission=5, size=8, num_objects=4, n_envs=65536, seed=42,
+                 env_index_offset=0, n_stack=4, all_doors_open=False, see_through_walls=True,
+                 obstacles=False, terminal_mode="truncated", mission_dtype=torch.int64,
+                 device="cuda", livelock_words=0, mt_table_words=0, reward64=False):
+        self.L = _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.MgxError("MgxEngine needs a GPU (no CPU fallback by design)")
+        self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        if problem not in _lib.PROBLEMS:
+            raise ValueError("Invalid problem type given: %s" % problem)
+        self.n = int(n_envs)
+        self.size = int(size)
+        self.n_stack = int(n_stack)
+        self.seed = int(seed)
+        self.env_index_offset = int(env_index_offset)
+        cfg = _lib.MgxConfig()
+        cfg.problem = _lib.PROBLEMS[problem]
+        cfg.mission = -1 if mission is None else int(mission)
+        cfg.size = self.size
+        cfg.num_objects = int(num_objects)
+        cfg.see_through_walls = int(bool(see_through_walls))
+        cfg.all_doors_open = int(bool(all_doors_open))
+        cfg.obstacles = int(bool(obstacles))
+        cfg.n_stack = self.n_stack
+        cfg.n_envs = self.n
+        cfg.base_seed = self.seed
+        cfg.env_index_offset = self.env_index_offset
+        cfg.livelock_words = int(livelock_words)
+        cfg.terminal_mode = _lib.TERMINAL[terminal_mode]
+        cfg.mission_int64 = 1 if mission_dtype == torch.int64 else 0
+        cfg.mt_table_words = int(mt_table_words)
+        self.terminal_mode = terminal_mode
+        self.mission_dtype = torch.int64 if cfg.mission_int64 else torch.uint8
+        h = _P()
+        _lib.check(self.L.mgx_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)), "mgx_create")
+        self.h = h
+        n, k, dev = self.n, self.n_stack, self.device
+        self.obs = dict(image=torch.zeros((n, 3 * k, 7, 7), dtype=torch.uint8, device=dev),
+                        direction=torch.zeros((n, 4 * k), dtype=torch.uint8, device=dev),
+                        mission=torch.zeros((n, 32 * k), dtype=self.mission_dtype, device=dev))
+        if terminal_mode != "none":
+            self.terminal_obs = {kk: torch.zeros_like(v) for kk, v in self.obs.items()}
+        else:
+            self.terminal_obs = None
+        self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.reward64 = torch.zeros(n, dtype=torch.float64, device=dev) if reward64 else None
+        self.terminated = torch.zeros(n, dtype=torch.bool, device=dev)
+        self.truncated = torch.zeros(n, dtype=torch.bool, device=dev)
+        self.done = torch.zeros(n, dtype=torch.bool, device=dev)
+        self.ep_return = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.livelock = torch.zeros(n, dtype=torch.int32, device=dev)
+        self._obs_c = _lib.MgxObs(_ptr(self.obs["image"]), _ptr(self.obs["direction"]), _ptr(self.obs["mission"]))
+        so = _lib.MgxStepOut()
+        so.obs = self._obs_c
+        if self.terminal_obs is not None:
+            so.terminal = _lib.MgxObs(_ptr(self.terminal_obs["image"]), _ptr(self.terminal_obs["direction"]),
+                                      _ptr(self.terminal_obs["mission"]))
+        so.reward_dev = _ptr(self.reward)
+        so.reward64_dev = _ptr(self.reward64)
+        so.terminated_dev = _ptr(self.terminated)
+        so.truncated_dev = _ptr(self.truncated)
+        so.done_dev = _ptr(self.done)
+        so.ep_return_dev = _ptr(self.ep_return)
+        so.ep_len_dev = _ptr(self.ep_len)
+        so.livelock_dev = _ptr(self.livelock)
+        self._step_out = so
+
+    # ------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self):
+        """First (seeded) reset: env i <- seed + env_index_offset + i."""
+        _lib.check(self.L.mgx_reset(self.h, ctypes.byref(self._obs_c), _ptr(self.livelock), self._stream()),
+                   "mgx_reset")
+        return self.obs
+
+    def step(self, actions):
+        """actions: int32/int64 device tensor [N].  Returns the in-place obs dict;
+        reward/terminated/truncated/done/ep_return/ep_len are attributes."""
+        if actions.device != self.device or actions.dtype not in (torch.int32, torch.int64) \
+                or actions.shape != (self.n,) or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous int32/int64 [%d] tensor on %s" % (self.n, self.device))
+        _lib.check(self.L.mgx_step(self.h, _ptr(actions), actions.element_size(), ctypes.byref(self._step_out),
+                                   self._stream()), "mgx_step")
+        return self.obs
+
+    def poll_error(self):
+        bits = ctypes.c_uint32()
+        _lib.check(self.L.mgx_poll_error(self.h, self._stream(), ctypes.byref(bits)), "mgx_poll_error")
+        if bits.value:
+            msgs = [m for b, m in _lib.DEVERR.items() if bits.value & b]
+            raise _lib.MgxError("device error: " + "; ".join(msgs))
+
+    def stats(self):
+        out = (ctypes.c_uint64 * 4)()
+        _lib.check(self.L.mgx_stats(self.h, self._stream(), out), "mgx_stats")
+        return dict(steps=int(out[0]), resets=int(out[1]), livelocks=int(out[2]), max_mt_cursor=int(out[3]))
+
+    def dump_state(self):
+        import numpy as np
+        n, S = self.n, self.size
+        out = dict(grid=np.zeros((n, S, S, 4), np.uint8), agent=np.zeros((n, 3), np.uint8),
+                   carrying=np.zeros((n, 4), np.uint8), step_count=np.zeros(n, np.int32),
+                   mission_done=np.zeros(n, np.uint8), stored_reward=np.zeros(n, np.float64),
+                   mtwords=np.zeros(n, np.int64), pcg=np.zeros((n, 6), np.uint64),
+                   target=np.zeros((n, 3), np.uint8), mission_id=np.zeros(n, np.uint8))
+        args = [out[k].ctypes.data_as(_P) for k in ("grid", "agent", "carrying", "step_count", "mission_done",
+                                                     "stored_reward", "mtwords", "pcg", "target", "mission_id")]
+        _lib.check(self.L.mgx_dump_state(self.h, self._stream(), *args), "mgx_dump_state")
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            torch.cuda.synchronize(self.device)
+            self.L.mgx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lambda, stats=None):
+    """DictRolloutBuffer.compute_returns_and_advantage on device (libmgx mgx_gae).
+
+    rewards/values/episode_starts: f32 [T, N]; last_values f32 [N]; last_dones bool/u8 [N].
+    Returns (advantages, returns) f32 [T, N].  `stats` (f64 [3] tensor, optional)
+    accumulates (sum A, sum A^2, count)."""
+    L = _lib.load()
+    T, N = rewards.shape
+    for t in (rewards, values, episode_starts):
+        assert t.dtype == torch.float32 and t.is_contiguous() and t.shape == (T, N)
+    lv = last_values.reshape(N).float().contiguous()
+    ld = last_dones.reshape(N).to(torch.uint8).contiguous()
+    adv = torch.empty_like(rewards)
+    ret = torch.empty_like(rewards)
+    gl = float(torch.tensor(gamma * gae_lambda, dtype=torch.float64).float())   # f32(gamma*lambda in fp64)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
+    _lib.check(L.mgx_gae(_ptr(rewards), _ptr(values), _ptr(episode_starts), _ptr(lv), _ptr(ld), T, N,
+                         ctypes.c_float(gamma), ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats), stream),
+               "mgx_gae")
+    return adv, ret

@@ -1,0 +1,214 @@
+"""HIP engine parity (needs an MI355X): libmgx through its C ABI against
+  (1) the golden fixtures made by executing the reference (all 19 configs,
+      every step, every state field, every RNG position),
+  (2) the SB3-layer oracle (VecTransposeImage + VecFrameStack + terminal obs),
+  (3) the C oracle at 1,024 envs (bit-exact transitions),
+  (4) the GAE oracle (bit-exact fp32),
+  (5) size-independent properties at the BASELINE size (65,536 envs).
+"""
+import numpy as np
+import pytest
+
+import trajcheck as TC
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+class EngineSource:
+    """libmgx behind trajcheck's compare() protocol (raw frames recovered from
+    the stacked, transposed observation)."""
+
+    def __init__(self, cfg, n_stack=4, mission_dtype=None):
+        from mgx import MgxEngine
+        kw = dict(cfg)
+        self.n = kw.pop("n_envs")
+        self.e = MgxEngine(n_envs=self.n, n_stack=n_stack, terminal_mode="all", reward64=True,
+                           mission_dtype=mission_dtype or torch.int64, **kw)
+        self.fs = None
+
+    @staticmethod
+    def newest(obs):
+        img = obs["image"][:, -3:].permute(0, 2, 3, 1).contiguous().cpu().numpy()
+        d = obs["direction"][:, -4:].argmax(1).to(torch.uint8).cpu().numpy()
+        m = obs["mission"][:, -32:].to(torch.uint8).cpu().numpy()
+        return img, d, m
+
+    def reset(self):
+        obs = self.e.reset()
+        img, d, m = self.newest(obs)
+        return dict(image=img, dir=d, mission=m, livelock=self.e.livelock.cpu().numpy())
+
+    def step(self, a):
+        obs = self.e.step(torch.as_tensor(a, device=self.e.device))
+        done = self.e.done.cpu().numpy()
+        img, d, m = self.newest(obs)
+        timg, td, tm = self.newest(self.e.terminal_obs)
+        dd = done.astype(bool)
+        return dict(image=np.where(dd[:, None, None, None], timg, img), dir=np.where(dd, td, d),
+                    mission=np.where(dd[:, None], tm, m), reward=self.e.reward64.cpu().numpy(),
+                    terminated=self.e.terminated.cpu().numpy().astype(np.uint8),
+                    truncated=self.e.truncated.cpu().numpy().astype(np.uint8),
+                    r_image=img, r_dir=d, r_mission=m, livelock=self.e.livelock.cpu().numpy())
+
+    def dump(self):
+        return self.e.dump_state()
+
+
+FIXTURES = TC.fixtures()
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=lambda p: p.split("/")[-1][:-4])
+def test_engine_matches_reference_fixture(path):
+    _need_gpu()
+    d = dict(np.load(path))
+    cfg, T = TC.fixture_cfg(d)
+    src = EngineSource(cfg)
+    msg = TC.compare(src, d)
+    src.e.poll_error()
+    assert msg is None, msg
+
+
+@pytest.mark.parametrize("name,n_stack,mdt", [("multi_all_s8", 4, "i64"), ("multi_pkp_s11", 3, "u8"),
+                                              ("multi_tgl_s16", 1, "i64")])
+def test_frame_stack_and_terminal_obs_match_sb3_layer(name, n_stack, mdt):
+    """Full stacked observation + stacked terminal_observation every step vs the
+    numpy VecTransposeImage/VecFrameStack restatement fed with the fixture."""
+    _need_gpu()
+    import oracle as O
+    d = dict(np.load(TC.GOLDEN + "/traj/%s.npz" % name))
+    cfg, T = TC.fixture_cfg(d)
+    n = cfg["n_envs"]
+    src = EngineSource(cfg, n_stack=n_stack, mission_dtype=torch.int64 if mdt == "i64" else torch.uint8)
+    fs = O.FrameStackOracle(n, n_stack)
+
+    def raw(img, dr, mi):
+        return dict(image=O.vec_transpose_image(img), direction=O.one_hot_dir(dr), mission=mi.astype(np.int64))
+
+    want = fs.reset(raw(d["reset0_image"], d["reset0_dir"], d["reset0_mission"]))
+    obs = src.e.reset()
+
+    def same(got, want):
+        return all(np.array_equal(got[k].to(torch.int64).cpu().numpy(), want[k].astype(np.int64)) for k in want)
+
+    assert same(obs, want)
+    for t in range(min(T, 200)):
+        done = (d["terminated"][t] | d["truncated"][t]).astype(bool)
+        step_obs = raw(np.where(done[:, None, None, None], d["r_image"][t], d["image"][t]),
+                       np.where(done, d["r_dir"][t], d["dir"][t]),
+                       np.where(done[:, None], d["r_mission"][t], d["mission"][t]))
+        term_frame = raw(d["image"][t], d["dir"][t], d["mission"][t])
+        want, want_term = fs.step(step_obs, done, term_frame)
+        obs = src.e.step(torch.as_tensor(d["actions"][t].astype(np.int64), device=src.e.device))
+        assert same(obs, want), "t=%d stacked obs" % t
+        if done.any():
+            for k in want_term:
+                got = src.e.terminal_obs[k].to(torch.int64).cpu().numpy()[done]
+                assert np.array_equal(got, want_term[k][done].astype(np.int64)), "t=%d terminal %s" % (t, k)
+    src.e.poll_error()
+
+
+@pytest.mark.parametrize("problem,mission,size", [("multi", 5, 8), ("multi", None, 8), ("multi", 2, 8),
+                                                  ("multi", None, 16), ("gto", None, 8)])
+def test_engine_matches_oracle_1024_envs(problem, mission, size):
+    """Bit-exact transitions vs the C oracle at 1,024 envs x 256 random steps
+    (global env index offset 4096 exercises sharded seeding)."""
+    _need_gpu()
+    import oracle as O
+    from mgx import MgxEngine
+    n, T, off = 1024, 256, 4096
+    ov = O.OracleVec(problem, mission, size, 4, n, 42, index_offset=off)
+    eng = MgxEngine(problem=problem, mission=mission, size=size, n_envs=n, env_index_offset=off, n_stack=4,
+                    terminal_mode="all", reward64=True)
+    r = ov.reset()
+    obs = eng.reset()
+    img, dr, mi = EngineSource.newest(obs)
+    assert np.array_equal(img, r["image"]) and np.array_equal(dr, r["dir"]) and np.array_equal(mi, r["mission"])
+    acts = np.random.default_rng(99).integers(0, 7, (T, n))
+    for t in range(T):
+        o = ov.step(acts[t])
+        obs = eng.step(torch.as_tensor(acts[t], device=eng.device))
+        done = eng.done.cpu().numpy().astype(bool)
+        assert np.array_equal(done, (o["terminated"] | o["truncated"]).astype(bool)), t
+        assert np.array_equal(eng.reward64.cpu().numpy(), o["reward"]), t
+        assert np.array_equal(eng.reward.cpu().numpy(), o["reward"].astype(np.float32)), t
+        img, dr, mi = EngineSource.newest(obs)
+        timg, tdr, tmi = EngineSource.newest(eng.terminal_obs)
+        assert np.array_equal(np.where(done[:, None, None, None], timg, img), o["image"]), t
+        assert np.array_equal(img[done], o["r_image"][done]), t
+        assert np.array_equal(np.where(done, tdr, dr), o["dir"]), t
+        assert np.array_equal(np.where(done[:, None], tmi, mi), o["mission"]), t
+        assert np.array_equal(eng.livelock.cpu().numpy()[done], o["livelock"][done]), t
+    a, b = eng.dump_state(), ov.dump()
+    for k in ("grid", "agent", "carrying", "step_count", "mission_done", "mtwords", "pcg", "target"):
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a["stored_reward"], b["stored_reward"], equal_nan=True)
+    eng.poll_error()
+
+
+def test_gae_bit_exact():
+    _need_gpu()
+    import oracle as O
+    from mgx import gae
+    rng = np.random.default_rng(5)
+    T, N = 64, 4099
+    r = rng.standard_normal((T, N)).astype(np.float32)
+    v = rng.standard_normal((T, N)).astype(np.float32)
+    es = (rng.random((T, N)) < 0.15).astype(np.float32)
+    lv = rng.standard_normal(N).astype(np.float32)
+    ld = rng.random(N) < 0.2
+    g, lam = 0.8108071290665859, 0.9452281119742252
+    want_a, want_r = O.gae(r, v, es, lv, ld, g, lam)
+    dev = torch.device("cuda")
+    st = torch.zeros(3, dtype=torch.float64, device=dev)
+    a, ret = gae(torch.tensor(r, device=dev), torch.tensor(v, device=dev), torch.tensor(es, device=dev),
+                 torch.tensor(lv, device=dev), torch.tensor(ld, device=dev), g, lam, stats=st)
+    assert np.array_equal(a.cpu().numpy(), want_a)
+    assert np.array_equal(ret.cpu().numpy(), want_r)
+    s = st.cpu().numpy()
+    assert s[2] == T * N
+    assert abs(s[0] - want_a.astype(np.float64).sum()) < 1e-6 * abs(want_a).sum()
+
+
+def test_baseline_size_properties():
+    """65,536 envs (BASELINE config 2): invariants that hold at any size --
+    determinism across two engines, a 64-env sample equal to the oracle,
+    well-formed observations, monotone step counters."""
+    _need_gpu()
+    import oracle as O
+    from mgx import MgxEngine
+    n, T = 65536, 64
+    e1 = MgxEngine(problem="multi", mission=5, size=8, n_envs=n)
+    e2 = MgxEngine(problem="multi", mission=5, size=8, n_envs=n)
+    e1.reset()
+    e2.reset()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    acts_log = []
+    for t in range(T):
+        a = torch.randint(0, 7, (n,), device="cuda", generator=g)
+        acts_log.append(a.cpu().numpy())
+        o1 = e1.step(a)
+        o2 = e2.step(a)
+    for k in o1:
+        assert torch.equal(o1[k], o2[k]), k
+    img = o1["image"].view(n, 4, 3, 7, 7)[:, -1]
+    assert int(img[:, 0].max()) <= 10 and int(img[:, 1].max()) <= 5 and int(img[:, 2].max()) <= 2
+    assert torch.all(o1["direction"].view(n, 4, 4)[:, -1].sum(1) == 1)
+    # sample: envs [1000, 1064) equal the oracle (global index offset 1000)
+    ov = O.OracleVec("multi", 5, 8, 4, 64, 42, index_offset=1000)
+    ov.reset()
+    for t in range(T):
+        ov.step(acts_log[t][1000:1064])
+    a_, b_ = e1.dump_state(), ov.dump()
+    for k in ("grid", "agent", "step_count", "mtwords", "pcg"):
+        assert np.array_equal(a_[k][1000:1064], b_[k]), k
+    st = e1.stats()
+    assert st["steps"] == n * T and st["resets"] > n
+    e1.poll_error()
