@@ -1,0 +1,206 @@
+"""bench.py -- env-steps/s of the MI355X MiniGrid engine (BASELINE config 2).
+
+Workload (one "step" = one vectorised step of the whole per-GPU batch through
+the drop-in path: PlaygroundEnv.step + gen_obs + VecTransposeImage +
+VecFrameStack(4) roll + SubprocVecEnv auto-reset, i.e. one `mgx_step`):
+  multi / mission 5 ('go to goal', GTG) / 8x8 / num_objects 4 / 65,536 envs per
+  GPU, uniform random actions on {0..6} (pre-generated on device for all
+  warmup+timed steps, so inputs are resident in HBM), seed 42, env global
+  index i seeded 42+i (rank r owns [r*N, (r+1)*N)) -> weak scaling.
+
+Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel
+(mgx_step_kernel) with SURVEY.md §8(d)'s algorithmic bytes
+  B_alg = 334*steps + (3*S^2 + 208)*resets
+divided by its average launch time measured with HIP events on the launch
+stream; `traffic` is the rocprofv3 PMC figure committed under profiles/.
+`cpu_baseline` times the C oracle (oracle/, single thread) on a bounded sample.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "minigrid-rl_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "env-steps/sec at 65k parallel envs, 1/2/4/8 MI355X; % HBM roofline"
+PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+B_STEP = 334                    # per env-step algorithmic bytes
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2048)
+    ap.add_argument("--warmup", type=int, default=128)
+    ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--problem", default="multi")
+    ap.add_argument("--mission", default="5")
+    ap.add_argument("--size", type=int, default=8)
+    ap.add_argument("--n-stack", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, seconds):
+    """C oracle (oracle/libmgx_oracle.so), one thread, same config, bounded sample."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    n = 1024
+    mission = None if args.mission == "None" else int(args.mission)
+    v = O.OracleVec(args.problem, mission, args.size, 4, n, 42)
+    v.reset()
+    rng = np.random.default_rng(1234)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        acts = rng.integers(0, 7, (16, n)).astype(np.int32)
+        for k in range(16):
+            v.step(acts[k])
+        steps += 16
+    dt = time.perf_counter() - t0
+    return dict(value=n * steps / dt, unit="env-steps/s", cores=1, kind="port",
+                sample="C oracle (oracle/mgx_oracle.c), 1 thread, %d envs x %d steps (%.1fs), same config, "
+                       "auto-reset included; host: %s" % (n, steps, dt, _cpu_model()))
+
+
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from mgx import MgxEngine
+
+    n = args.n_envs
+    mission = None if args.mission == "None" else int(args.mission)
+    eng = MgxEngine(problem=args.problem, mission=mission, size=args.size, n_envs=n, seed=42,
+                    env_index_offset=rank * n, n_stack=args.n_stack, terminal_mode="truncated", device=dev)
+    K, W = args.steps, args.warmup
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    actions = torch.randint(0, 7, (W + K, n), device=dev, generator=g, dtype=torch.int32)
+    eng.reset()
+    stream = torch.cuda.current_stream(dev)
+    for t in range(W):
+        eng.step(actions[t])
+    torch.cuda.synchronize(dev)
+    graph = None
+    if args.graph:
+        # capture the K timed steps once (launch-bound loop -> one hipGraph replay)
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            graph.capture_begin()
+            for t in range(K):
+                eng.step(actions[W + t])
+            graph.capture_end()
+        torch.cuda.synchronize(dev)
+        # graph capture did not execute: re-seed so timed steps continue from the warmup state
+    st0 = eng.stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    if graph is not None:
+        ev0.record(stream)
+        graph.replay()
+        ev1.record(stream)
+    else:
+        ev0.record(stream)
+        for t in range(K):
+            eng.step(actions[W + t])
+        ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    st1 = eng.stats()
+    eng.poll_error()
+    elapsed = torch.tensor([wall, gpu_ms / 1e3], dtype=torch.float64, device=dev)
+    steps_done = torch.tensor([float(st1["steps"] - st0["steps"]), float(st1["resets"] - st0["resets"])],
+                              dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(steps_done, op=dist.ReduceOp.SUM)
+    wall_max, gpu_max = float(elapsed[0]), float(elapsed[1])
+    total_env_steps, total_resets = float(steps_done[0]), float(steps_done[1])
+    assert int(total_env_steps) == n * K * world, (total_env_steps, n * K * world)
+    if rank == 0:
+        per_launch_s = float(gpu_ms) / 1e3 / K                       # rank-0 kernel time per launch
+        resets_per_launch = (st1["resets"] - st0["resets"]) / K
+        b_alg = B_STEP * n + (3 * args.size ** 2 + 208) * resets_per_launch
+        achieved = b_alg / per_launch_s / 1e9
+        traffic = None
+        if os.path.exists(PMC_FILE):
+            try:
+                pmc = json.load(open(PMC_FILE))
+                if pmc.get("n_envs") == n and pmc.get("size") == args.size and pmc.get("mission") == mission:
+                    traffic = pmc.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        stack_bytes = n * (441 + 588 + 12 + 16)   # VecFrameStack image + direction roll (reported separately)
+        out = {
+            "metric": METRIC,
+            "value": total_env_steps / wall_max,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": wall_max * 1e3 / K,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (uniform random actions on {0..6}, seed 1234+rank; env i seeded 42+i)",
+            "config": {"workload": "GTG 8x8 random-action rollout, %d envs/GPU (BASELINE config 2)" % n
+                       if (args.problem, mission, args.size) == ("multi", 5, 8) else
+                       "%s/%s %dx%d random-action rollout, %d envs/GPU" % (args.problem, mission, args.size,
+                                                                           args.size, n),
+                       "problem": args.problem, "mission": mission, "size": args.size, "num_objects": 4,
+                       "envs_per_gpu": n, "n_stack": args.n_stack, "parallelism": "env-sharded dp%d" % world,
+                       "hipgraph": bool(graph is not None)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
+                         "kernel": "mgx_step_kernel", "avg_launch_us": per_launch_s * 1e6,
+                         "alg_bytes_per_launch": b_alg, "resets_per_launch": resets_per_launch,
+                         "stack_bytes_per_launch": stack_bytes,
+                         "achieved_incl_stack": (b_alg + stack_bytes) / per_launch_s / 1e9},
+            "gpu_time_ms": gpu_max * 1e3,
+        }
+        if args.cpu_seconds > 0 and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

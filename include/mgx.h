@@ -136,8 +136,10 @@ mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const floa
 mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits);
 
 /* Counters since create: [0] env-steps, [1] resets (incl. first), [2] abandoned
- * (live-locked) reset attempts, [3] max MT cursor.  Synchronises `stream`. */
-mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[4]);
+ * (live-locked) reset attempts, [3] max MT cursor, [4..7] per-phase shader-clock
+ * sums of mgx_step_kernel (non-zero only in a -DMGX_STAMPS diagnostic build).
+ * Synchronises `stream`. */
+mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]);
 
 /* Test/debug: copy env state to HOST buffers (any may be NULL); synchronises.
  * grid u8 [N][S][S][4] (x-major (type,colour,state,box-holds-key)), agent u8 [N][3],

@@ -166,7 +166,7 @@ __device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t &hc) {
 __device__ __forceinline__ uint32_t ss_mix(uint32_t x, uint32_t y) {
     uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y; r ^= r >> 16; return r;
 }
-__device__ inline void pcg_seed(Pcg &p, uint64_t seed) {
+__device__ __forceinline__ void pcg_seed(Pcg &p, uint64_t seed) {
     uint32_t e0 = (uint32_t)seed, e1 = (uint32_t)(seed >> 32);
     int nent = (seed >> 32) ? 2 : 1;
     uint32_t pool[4];
@@ -202,8 +202,9 @@ __device__ inline void pcg_seed(Pcg &p, uint64_t seed) {
 
 // ------------------------------------------------------------ generator context
 constexpr int MT_WIN = 64;        // words per lane-private LDS window
-constexpr int WIN_STRIDE = 68;    // words; 68 mod 32 = 4 -> b128 writes spread over banks
+constexpr int WIN_STRIDE = 65;    // words per lane window (odd -> lane-private rows hit distinct banks)
 constexpr int MAX_OBJS = 32;
+constexpr int OBJ_STRIDE = 33;    // words per lane objs list (odd, same reason)
 constexpr int SAT_PROBE = 64;     // rejections before the exhaustive satisfiability probe
 constexpr uint32_t PCG_LOOP_LIMIT = 1u << 20;
 
@@ -228,16 +229,21 @@ struct Gen {
 
 __device__ __forceinline__ uint8_t &cell(Gen &G, int x, int y) { return G.g[y * G.S + x]; }
 
-// Refill the lane's LDS window with table[cur & ~3 .. +MT_WIN) (16 independent
-// 16-B loads in flight, one HBM/L2 round trip per window).
+// Refill the lane's LDS window with table[cur & ~3 .. +MT_WIN): 16 independent
+// 16-B global loads in flight (one L2/HBM round trip), 64 dword LDS stores
+// (the window row is 4-B aligned: odd dword stride avoids bank conflicts).
 __device__ __forceinline__ uint64_t mt_refill(const uint32_t *__restrict__ table, uint64_t tlen, uint32_t *win,
                                               uint64_t cur, uint32_t &err) {
     uint64_t base = cur & ~3ull;
     if (base + MT_WIN > tlen) { err |= 1u; base = tlen; }   // MGX_DEVERR_MT_TABLE: read the zero pad
     const uint4 *src = reinterpret_cast<const uint4 *>(table + base);
-    uint4 *dst = reinterpret_cast<uint4 *>(win);
+    uint4 v[MT_WIN / 4];
 #pragma unroll
-    for (int k = 0; k < MT_WIN / 4; k++) dst[k] = src[k];
+    for (int k = 0; k < MT_WIN / 4; k++) v[k] = src[k];
+#pragma unroll
+    for (int k = 0; k < MT_WIN / 4; k++) {
+        win[4 * k] = v[k].x; win[4 * k + 1] = v[k].y; win[4 * k + 2] = v[k].z; win[4 * k + 3] = v[k].w;
+    }
     return base;
 }
 
@@ -276,7 +282,7 @@ __device__ __forceinline__ void add_obj(Gen &G, int t, int cname, int x, int y) 
 }
 
 // MiniGridEnv.place_obj(obj) over the whole grid (PCG64)
-__device__ inline void place_obj_any(Gen &G, uint8_t code, int &px, int &py) {
+__device__ __forceinline__ void place_obj_any(Gen &G, uint8_t code, int &px, int &py) {
     for (uint32_t it = 0;; ++it) {
         if (it > PCG_LOOP_LIMIT) { G.err |= 4u; px = 1; py = 1; return; }
         int x = pcg_integers(G.pcg, 0, G.S);
@@ -288,7 +294,7 @@ __device__ inline void place_obj_any(Gen &G, uint8_t code, int &px, int &py) {
         return;
     }
 }
-__device__ inline void place_agent(Gen &G) {
+__device__ __forceinline__ void place_agent(Gen &G) {
     G.ax = -1; G.ay = -1;
     int x, y;
     place_obj_any(G, CODE_EMPTY, x, y);
@@ -315,7 +321,7 @@ __device__ __forceinline__ void live_lock(Gen &G) {
 
 // `while True: p=(randint(x0,x1), randint(y0,y1)); if p!=goal and [p!=agent] and
 //  [p!=other] and not next2door(p): break` -> grid.set(Box(c,Key(c)) | Key(c)); objs.append
-__device__ inline void place_key(Gen &G, int x0, int x1, int y0, int y1, int gx, int gy, bool chk_agent,
+__device__ __forceinline__ void place_key(Gen &G, int x0, int x1, int y0, int y1, int gx, int gy, bool chk_agent,
                                  int ox, int oy, int cname, bool kib, int *kx, int *ky) {
     int x, y, rej = 0;
     for (;;) {
@@ -343,7 +349,7 @@ __device__ inline void place_key(Gen &G, int x0, int x1, int y0, int y1, int gx,
 // `for _ in range(n): (t,c)=choice(obj_choice); obj_choice.remove((t,c)); while True:
 //  p=(randint..); [p in objs -> retry]; if p != agent and not next2door(p): break; put_obj`
 // (p in objs <=> grid cell occupied, inside a room interior)
-__device__ inline void place_objects(Gen &G, uint32_t &oc, const int *types, int n, int x0, int x1,
+__device__ __forceinline__ void place_objects(Gen &G, uint32_t &oc, const int *types, int n, int x0, int x1,
                                      int y0, int y1) {
     for (int k = 0; k < n; k++) {
         if (oc == 0) { G.err |= 8u; return; }
@@ -371,7 +377,7 @@ __device__ inline void place_objects(Gen &G, uint32_t &oc, const int *types, int
     }
 }
 
-__device__ inline void place_goal_multi(Gen &G, int &gx, int &gy) {
+__device__ __forceinline__ void place_goal_multi(Gen &G, int &gx, int &gy) {
     for (uint32_t it = 0;; ++it) {
         if (it > PCG_LOOP_LIMIT) { G.err |= 4u; break; }
         place_obj_any(G, CODE_GOAL, gx, gy);
@@ -385,192 +391,147 @@ __device__ __forceinline__ int door_code(int cname, bool locked, bool open) {
     return open ? mk_code(T_OPEN, cn2idx(cname), 0) : mk_code(T_DOOR, cn2idx(cname), locked ? 1 : 0);
 }
 
-// obj_choice removal when a door is locked: bits ('key', c) = c, ('box', c) = 12 + c
-struct DoorDraw { int col; bool lk, kib; };
-__device__ inline DoorDraw draw_door(Gen &G, uint32_t &dcols, uint32_t &oc) {
-    DoorDraw d;
-    d.col = mask_choice(G, dcols);
-    dcols &= ~(1u << d.col);
-    d.lk = G.all_doors_open ? false : choice_bool(G);
-    d.kib = choice_bool(G);
-    if (d.lk) { oc &= ~(1u << d.col); if (d.kib) oc &= ~(1u << (12 + d.col)); }
-    return d;
+// ---- multi-room layouts, table-driven (custom_env.py:617-2034) ---------------
+// One generic pass reproduces _generate_2/3/4_rooms: same RNG draws in the same
+// order, same Q1/Q5 quirks, one call site per primitive (keeps the generator
+// in registers).  Doors are indexed in the reference's draw order:
+//   2 rooms: 0 = vertical door;  3 rooms: 0 = h, 1 = vu, 2 = vl;
+//   4 rooms: 0 = hl, 1 = hr, 2 = vu, 3 = vl.
+// Rooms are visited in the reference's order:
+//   2: L, R;  3: UL, LL, R;  4: UL, LL, UR, LR.
+
+// door d of an nr-room layout: bit0 = horizontal (x drawn, y = mid); range lo..hi
+__device__ __forceinline__ void door_geom(int nr, int d, int mid, int S, bool &horiz, int &lo, int &hi) {
+    if (nr == 2) { horiz = false; lo = 1; hi = S - 2; return; }
+    if (nr == 3) {
+        horiz = d == 0;
+        lo = d == 2 ? mid + 1 : 1;
+        hi = d == 2 ? S - 2 : mid - 1;
+        return;
+    }
+    horiz = d < 2;
+    const bool upper_half = (d == 0 || d == 2);
+    lo = upper_half ? 1 : mid + 1;
+    hi = upper_half ? mid - 1 : S - 2;
 }
-__device__ inline void set_door(Gen &G, const DoorDraw &d, int x, int y) {
-    bool open = G.all_doors_open ? choice_bool(G) : false;
-    cell(G, x, y) = (uint8_t)door_code(d.col, d.lk, open);
-    add_obj(G, T_DOOR, d.col, x, y);
+
+__device__ __forceinline__ int room_of(int nr, int x, int y, int mid) {
+    const bool left = x < mid, up = y < mid;
+    if (nr == 2) return left ? 0 : 1;
+    if (nr == 3) return left ? (up ? 0 : 1) : 2;
+    return left ? (up ? 0 : 1) : (up ? 2 : 3);
+}
+
+__device__ __forceinline__ void room_rect(int nr, int r, int mid, int S, int &x0, int &x1, int &y0, int &y1) {
+    const bool left = (nr == 2) ? r == 0 : r <= 1;
+    const bool full_h = nr == 2 || (nr == 3 && r == 2);
+    const bool up = (r == 0) || (nr == 4 && r == 2);
+    x0 = left ? 1 : mid + 1; x1 = left ? mid - 1 : S - 2;
+    y0 = full_h ? 1 : (up ? 1 : mid + 1); y1 = full_h ? S - 2 : (up ? mid - 1 : S - 2);
+}
+
+// keys placed in room r given the agent's room ar: kA, kB door indices (-1 none);
+// chk = the agent-room form (agent + other-key checks)
+__device__ __forceinline__ void key_spec(int nr, int r, int ar, int &kA, int &kB, bool &chk) {
+    kA = -1; kB = -1; chk = (r == ar);
+    if (nr == 2) { if (r == ar) kA = 0; return; }
+    if (nr == 3) {
+        if (r != ar) return;
+        if (r == 0) { kA = 1; kB = 0; }        // UL: vu, h
+        else if (r == 1) { kA = 2; kB = 0; }   // LL: vl, h
+        else { kA = 2; kB = 1; }               // R : vl, vu
+        return;
+    }
+    const int HL = 0, HR = 1, VU = 2, VL = 3;
+    if (r == 0) {        // UL
+        if (ar == 0) { kA = VU; kB = HL; } else if (ar == 1) kA = VU; else if (ar == 2) kA = HL;
+    } else if (r == 1) { // LL
+        if (ar == 1) { kA = VL; kB = HL; } else if (ar == 3) kA = HL; else if (ar == 0) kA = VL;
+    } else if (r == 2) { // UR
+        if (ar == 2) { kA = VU; kB = HR; } else if (ar == 3) kA = VU; else if (ar == 0) kA = HR;
+    } else {             // LR
+        if (ar == 3) { kA = VL; kB = HR; } else if (ar == 1) kA = HR; else if (ar == 2) kA = VL;
+    }
 }
 
 __device__ const int MULTI_TYPES[3] = {T_KEY, T_BALL, T_BOX};
 
-__device__ inline void gen_2_rooms(Gen &G, int mid) {          // custom_env.py:617-855
-    const int S = G.S;
-    int n_left = G.num_objects / 2, n_right = G.num_objects - n_left;
-    uint32_t oc = 0x3FFFFu;
+__device__ __forceinline__ void gen_rooms(Gen &G, int nr) {
+    const int S = G.S, mid = S / 2;
     for (int i = 1; i < S - 1; i++) cell(G, mid, i) = CODE_WALL;
-    uint32_t dc = 0x3Fu;
-    DoorDraw d = draw_door(G, dc, oc);
+    if (nr == 3) for (int i = 1; i < mid; i++) cell(G, i, mid) = CODE_WALL;
+    if (nr == 4) for (int i = 1; i < S - 1; i++) cell(G, i, mid) = CODE_WALL;
+    const int ndoors = nr == 2 ? 1 : nr;
+    uint32_t oc = 0x3FFFFu;    // obj_choice: bit = type_slot*6 + colour-name (key, ball, box)
+    uint32_t dc = 0x3Fu;       // door_colors
+    uint32_t dinfo = 0;        // per door byte: colour | locked<<3 | key_in_box<<4
+    // colour / locked / key_in_box draws, door by door (custom_env.py:635-643, 878-908, 1322-1362)
+#pragma unroll 1
+    for (int d = 0; d < ndoors; d++) {
+        const int col = mask_choice(G, dc);
+        dc &= ~(1u << col);
+        const bool lk = G.all_doors_open ? false : choice_bool(G);
+        const bool kib = choice_bool(G);
+        if (lk) { oc &= ~(1u << col); if (kib) oc &= ~(1u << (12 + col)); }
+        dinfo |= (uint32_t)(col | (lk << 3) | (kib << 4)) << (8 * d);
+    }
     if (G.abort) return;
-    int j = randint(G, 1, S - 2);
-    set_door(G, d, mid, j);
+    // door positions (custom_env.py:646-650, 911-930, 1365-1391)
+#pragma unroll 1
+    for (int d = 0; d < ndoors; d++) {
+        bool horiz; int lo, hi;
+        door_geom(nr, d, mid, S, horiz, lo, hi);
+        const int v = randint(G, lo, hi);
+        const int x = horiz ? v : mid, y = horiz ? mid : v;
+        const uint32_t di = dinfo >> (8 * d);
+        const bool open = G.all_doors_open ? choice_bool(G) : false;
+        cell(G, x, y) = (uint8_t)door_code(di & 7, (di >> 3) & 1, open);
+        add_obj(G, T_DOOR, di & 7, x, y);
+    }
     if (G.abort) return;
     int gx, gy;
     place_goal_multi(G, gx, gy);
-    bool goal_left = gx < mid;
     place_agent(G);
-    bool a_left = G.ax < mid;
-    if (a_left && d.lk) { n_left--; place_key(G, 1, mid - 1, 1, S - 2, gx, gy, true, -1, -1, d.col, d.kib, 0, 0); }
-    if (G.abort) return;
-    if (goal_left) n_left--;
-    place_objects(G, oc, MULTI_TYPES, n_left, 1, mid - 1, 1, S - 2);
-    if (G.abort) return;
-    if (!a_left && d.lk) { n_right--; place_key(G, mid + 1, S - 2, 1, S - 2, gx, gy, true, -1, -1, d.col, d.kib, 0, 0); }
-    if (G.abort) return;
-    if (!goal_left) n_right--;
-    place_objects(G, oc, MULTI_TYPES, n_right, mid + 1, S - 2, 1, S - 2);
+    const int gr = room_of(nr, gx, gy, mid), ar = room_of(nr, G.ax, G.ay, mid);
+    // object counters: c0 = (left | upper-left), c1 = (right | lower-left, unused by Q1), c2, c3
+    const int n_left = G.num_objects / 2, n_right = G.num_objects - n_left;
+    int c0, c1, c2, c3;
+    if (nr == 2) { c0 = n_left; c1 = n_right; c2 = c3 = 0; }
+    else if (nr == 3) { c0 = n_left / 2; c1 = n_left - c0; c2 = n_right; c3 = 0; }
+    else { c0 = n_left / 2; c1 = n_left - c0; c2 = n_right / 2; c3 = n_right - c2; }
+#pragma unroll 1
+    for (int r = 0; r < nr; r++) {
+        int x0, x1, y0, y1;
+        room_rect(nr, r, mid, S, x0, x1, y0, y1);
+        int kA, kB;
+        bool chk;
+        key_spec(nr, r, ar, kA, kB, chk);
+        int ndec = 0;
+        int kx = -1, ky = -1;
+        if (kA >= 0 && ((dinfo >> (8 * kA + 3)) & 1)) {
+            const uint32_t di = dinfo >> (8 * kA);
+            ndec++;
+            place_key(G, x0, x1, y0, y1, gx, gy, chk, -1, -1, di & 7, (di >> 4) & 1, &kx, &ky);
+            if (G.abort) return;
+        }
+        if (kB >= 0 && ((dinfo >> (8 * kB + 3)) & 1)) {
+            const uint32_t di = dinfo >> (8 * kB);
+            ndec++;
+            place_key(G, x0, x1, y0, y1, gx, gy, chk, kx, ky, di & 7, (di >> 4) & 1, 0, 0);
+            if (G.abort) return;
+        }
+        if (gr == r) ndec++;
+        int n;
+        if (r == 0) { c0 -= ndec; n = c0; }
+        else if (r == 1) { c1 -= ndec; n = (nr == 2) ? c1 : c0; }   // Q1: lower-left loops over c0
+        else if (r == 2) { c2 -= ndec; n = c2; }
+        else { c3 -= ndec; n = c3; }
+        place_objects(G, oc, MULTI_TYPES, n, x0, x1, y0, y1);
+        if (G.abort) return;
+    }
 }
 
-__device__ inline void gen_3_rooms(Gen &G, int mid) {          // custom_env.py:857-1297
-    const int S = G.S;
-    int n_left = G.num_objects / 2;
-    int n_lu = n_left / 2, n_right = G.num_objects - n_left;
-    uint32_t oc = 0x3FFFFu;
-    for (int i = 1; i < S - 1; i++) cell(G, mid, i) = CODE_WALL;
-    for (int i = 1; i < mid; i++) cell(G, i, mid) = CODE_WALL;
-    uint32_t dc = 0x3Fu;
-    DoorDraw h = draw_door(G, dc, oc);
-    DoorDraw vu = draw_door(G, dc, oc);
-    DoorDraw vl = draw_door(G, dc, oc);
-    if (G.abort) return;
-    int h_i = randint(G, 1, mid - 1); set_door(G, h, h_i, mid);
-    int vu_j = randint(G, 1, mid - 1); set_door(G, vu, mid, vu_j);
-    int vl_j = randint(G, mid + 1, S - 2); set_door(G, vl, mid, vl_j);
-    if (G.abort) return;
-    int gx, gy;
-    place_goal_multi(G, gx, gy);
-    bool g_left = gx < mid, g_up = gy < mid;
-    place_agent(G);
-    bool a_left = G.ax < mid, a_up = G.ay < mid;
-    if (a_left && a_up) {      // upper left
-        int kx = -1, ky = -1;
-        if (vu.lk) { n_lu--; place_key(G, 1, mid - 1, 1, mid - 1, gx, gy, true, -1, -1, vu.col, vu.kib, &kx, &ky); }
-        if (G.abort) return;
-        if (h.lk) { n_lu--; place_key(G, 1, mid - 1, 1, mid - 1, gx, gy, true, kx, ky, h.col, h.kib, 0, 0); }
-        if (G.abort) return;
-    }
-    if (g_left && g_up) n_lu--;
-    place_objects(G, oc, MULTI_TYPES, n_lu, 1, mid - 1, 1, mid - 1);
-    if (G.abort) return;
-    if (a_left && !a_up) {     // lower left
-        int kx = -1, ky = -1;
-        if (vl.lk) { place_key(G, 1, mid - 1, mid + 1, S - 2, gx, gy, true, -1, -1, vl.col, vl.kib, &kx, &ky); }
-        if (G.abort) return;
-        if (h.lk) { place_key(G, 1, mid - 1, mid + 1, S - 2, gx, gy, true, kx, ky, h.col, h.kib, 0, 0); }
-        if (G.abort) return;
-    }
-    // Q1 (custom_env.py:1119): the lower-left loop runs num_left_upper_objects times
-    place_objects(G, oc, MULTI_TYPES, n_lu, 1, mid - 1, mid + 1, S - 2);
-    if (G.abort) return;
-    if (!a_left) {             // right
-        int kx = -1, ky = -1;
-        if (vl.lk) { n_right--; place_key(G, mid + 1, S - 2, 1, S - 2, gx, gy, true, -1, -1, vl.col, vl.kib, &kx, &ky); }
-        if (G.abort) return;
-        if (vu.lk) { n_right--; place_key(G, mid + 1, S - 2, 1, S - 2, gx, gy, true, kx, ky, vu.col, vu.kib, 0, 0); }
-        if (G.abort) return;
-    }
-    if (!g_left) n_right--;
-    place_objects(G, oc, MULTI_TYPES, n_right, mid + 1, S - 2, 1, S - 2);
-}
-
-__device__ inline void gen_4_rooms(Gen &G, int mid) {          // custom_env.py:1299-2034
-    const int S = G.S;
-    int n_left = G.num_objects / 2;
-    int n_lu = n_left / 2;
-    int n_right = G.num_objects - n_left;
-    int n_ru = n_right / 2, n_rl = n_right - n_ru;
-    uint32_t oc = 0x3FFFFu;
-    for (int i = 1; i < S - 1; i++) cell(G, mid, i) = CODE_WALL;
-    for (int i = 1; i < S - 1; i++) cell(G, i, mid) = CODE_WALL;
-    uint32_t dc = 0x3Fu;
-    DoorDraw hl = draw_door(G, dc, oc);
-    DoorDraw hr = draw_door(G, dc, oc);
-    DoorDraw vu = draw_door(G, dc, oc);
-    DoorDraw vl = draw_door(G, dc, oc);
-    if (G.abort) return;
-    int hl_i = randint(G, 1, mid - 1); set_door(G, hl, hl_i, mid);
-    int hr_i = randint(G, mid + 1, S - 2); set_door(G, hr, hr_i, mid);
-    int vu_j = randint(G, 1, mid - 1); set_door(G, vu, mid, vu_j);
-    int vl_j = randint(G, mid + 1, S - 2); set_door(G, vl, mid, vl_j);
-    if (G.abort) return;
-    int gx, gy;
-    place_goal_multi(G, gx, gy);
-    bool g_left = gx < mid, g_up = gy < mid;
-    place_agent(G);
-    bool a_left = G.ax < mid, a_up = G.ay < mid;
-    const int L0 = 1, L1 = mid - 1, R0 = mid + 1, R1 = S - 2;
-    // upper left (custom_env.py:1414-1530)
-    if (a_left && a_up) {
-        int kx = -1, ky = -1;
-        if (vu.lk) { n_lu--; place_key(G, L0, L1, L0, L1, gx, gy, true, -1, -1, vu.col, vu.kib, &kx, &ky); }
-        if (G.abort) return;
-        if (hl.lk) { n_lu--; place_key(G, L0, L1, L0, L1, gx, gy, true, kx, ky, hl.col, hl.kib, 0, 0); }
-    } else if (a_left && !a_up) {
-        if (vu.lk) { n_lu--; place_key(G, L0, L1, L0, L1, gx, gy, false, -1, -1, vu.col, vu.kib, 0, 0); }
-    } else if (!a_left && a_up) {
-        if (hl.lk) { n_lu--; place_key(G, L0, L1, L0, L1, gx, gy, false, -1, -1, hl.col, hl.kib, 0, 0); }
-    }
-    if (G.abort) return;
-    if (g_left && g_up) n_lu--;
-    place_objects(G, oc, MULTI_TYPES, n_lu, L0, L1, L0, L1);
-    if (G.abort) return;
-    // lower left (custom_env.py:1569-1685)
-    if (a_left && !a_up) {
-        int kx = -1, ky = -1;
-        if (vl.lk) { place_key(G, L0, L1, R0, R1, gx, gy, true, -1, -1, vl.col, vl.kib, &kx, &ky); }
-        if (G.abort) return;
-        if (hl.lk) { place_key(G, L0, L1, R0, R1, gx, gy, true, kx, ky, hl.col, hl.kib, 0, 0); }
-    } else if (!a_left && !a_up) {
-        if (hl.lk) { place_key(G, L0, L1, R0, R1, gx, gy, false, -1, -1, hl.col, hl.kib, 0, 0); }
-    } else if (a_left && a_up) {
-        if (vl.lk) { place_key(G, L0, L1, R0, R1, gx, gy, false, -1, -1, vl.col, vl.kib, 0, 0); }
-    }
-    if (G.abort) return;
-    // Q1 (custom_env.py:1660): the lower-left loop runs num_left_upper_objects times
-    place_objects(G, oc, MULTI_TYPES, n_lu, L0, L1, R0, R1);
-    if (G.abort) return;
-    // upper right (custom_env.py:1724-1841)
-    if (!a_left && a_up) {
-        int kx = -1, ky = -1;
-        if (vu.lk) { n_ru--; place_key(G, R0, R1, L0, L1, gx, gy, true, -1, -1, vu.col, vu.kib, &kx, &ky); }
-        if (G.abort) return;
-        if (hr.lk) { n_ru--; place_key(G, R0, R1, L0, L1, gx, gy, true, kx, ky, hr.col, hr.kib, 0, 0); }
-    } else if (!a_left && !a_up) {
-        if (vu.lk) { n_ru--; place_key(G, R0, R1, L0, L1, gx, gy, false, -1, -1, vu.col, vu.kib, 0, 0); }
-    } else if (a_left && a_up) {
-        if (hr.lk) { n_ru--; place_key(G, R0, R1, L0, L1, gx, gy, false, -1, -1, hr.col, hr.kib, 0, 0); }
-    }
-    if (G.abort) return;
-    if (!g_left && g_up) n_ru--;
-    place_objects(G, oc, MULTI_TYPES, n_ru, R0, R1, L0, L1);
-    if (G.abort) return;
-    // lower right (custom_env.py:1880-1997)
-    if (!a_left && !a_up) {
-        int kx = -1, ky = -1;
-        if (vl.lk) { n_rl--; place_key(G, R0, R1, R0, R1, gx, gy, true, -1, -1, vl.col, vl.kib, &kx, &ky); }
-        if (G.abort) return;
-        if (hr.lk) { n_rl--; place_key(G, R0, R1, R0, R1, gx, gy, true, kx, ky, hr.col, hr.kib, 0, 0); }
-    } else if (a_left && !a_up) {
-        if (hr.lk) { n_rl--; place_key(G, R0, R1, R0, R1, gx, gy, false, -1, -1, hr.col, hr.kib, 0, 0); }
-    } else if (!a_left && a_up) {
-        if (vl.lk) { n_rl--; place_key(G, R0, R1, R0, R1, gx, gy, false, -1, -1, vl.col, vl.kib, 0, 0); }
-    }
-    if (G.abort) return;
-    if (!g_left && !g_up) n_rl--;
-    place_objects(G, oc, MULTI_TYPES, n_rl, R0, R1, R0, R1);
-}
-
-__device__ inline int gen_multi(Gen &G) {                      // custom_env.py:595-615
+__device__ __forceinline__ int gen_multi(Gen &G) {             // custom_env.py:595-615
     int cmd;
     if (G.cfg_mission >= 0) cmd = G.cfg_mission;
     else {
@@ -578,12 +539,9 @@ __device__ inline int gen_multi(Gen &G) {                      // custom_env.py:
         cmd = r == 3 ? 5 : r;
     }
     if (G.abort) return 0;
-    int mid = G.S / 2;
-    int nr = randint(G, 2, 4);
+    const int nr = randint(G, 2, 4);
     if (G.abort) return 0;
-    if (nr == 2) gen_2_rooms(G, mid);
-    else if (nr == 3) gen_3_rooms(G, mid);
-    else gen_4_rooms(G, mid);
+    gen_rooms(G, nr);
     return cmd;
 }
 
@@ -592,7 +550,7 @@ __device__ const int GTG_T[4] = {T_BOX, T_DOOR, T_KEY, T_BALL};
 __device__ const int OPN_T[2] = {T_BOX, T_DOOR};
 __device__ const int PKP_T[3] = {T_KEY, T_BOX, T_BALL};
 
-__device__ inline int gen_single(Gen &G) {                     // custom_env.py:371-513
+__device__ __forceinline__ int gen_single(Gen &G) {                     // custom_env.py:371-513
     const int *types;
     int ntypes, cmd;
     bool goal = false;
@@ -628,7 +586,7 @@ struct ResetOut {
 };
 
 // One attempt of MiniGridEnv.reset -> PlaygroundEnv._gen_grid (custom_env.py:122-267).
-__device__ inline void gen_attempt(Gen &G, ResetOut &R) {
+__device__ __forceinline__ void gen_attempt(Gen &G, ResetOut &R) {
     const int S = G.S;
     for (int i = 0; i < S * S; i++) G.g[i] = CODE_EMPTY;
     for (int i = 0; i < S; i++) {                                 // wall_rect(0, 0, W, H)
@@ -679,7 +637,7 @@ __device__ inline void gen_attempt(Gen &G, ResetOut &R) {
 }
 
 // MiniGridEnv.reset with the engine's live-lock retry policy.
-__device__ inline void reset_env(Gen &G, ResetOut &R) {
+__device__ __forceinline__ void reset_env(Gen &G, ResetOut &R) {
     R.livelocks = 0;
     for (;;) {
         G.astart = G.cur;

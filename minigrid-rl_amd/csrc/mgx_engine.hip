@@ -34,7 +34,7 @@ namespace {
 constexpr int BLOCK_ENVS = 64;
 constexpr int BLOCK_THREADS = 256;
 constexpr int FRAME = 147;                 // 3 x 7 x 7
-constexpr int SCRATCH_PER_ENV = WIN_STRIDE * 4 + MAX_OBJS * 4;   // LDS bytes per resetting lane
+constexpr int SCRATCH_PER_ENV = WIN_STRIDE * 4 + OBJ_STRIDE * 4;   // LDS bytes per resetting lane
 
 struct KParams {
     EnvState *state;
@@ -48,7 +48,7 @@ struct KParams {
     uint64_t tlen;
     int64_t n;
     int64_t seed_base;              // base_seed + env_index_offset
-    int S, GS, n_stack, img_bytes, stk_lds, problem, cfg_mission, num_objects, all_doors_open;
+    int S, GS, GSL, n_stack, img_bytes, stk_lds, problem, cfg_mission, num_objects, all_doors_open;
     uint32_t llw;
     int terminal_mode, mission64;
 };
@@ -66,32 +66,54 @@ struct KOut {
     int32_t *livelock;
 };
 
-__device__ __forceinline__ void coop_copy_in(uint8_t *__restrict__ lds, const uint8_t *__restrict__ g, int nbytes) {
-    const int n16 = nbytes >> 4;
+// Grids: global rows are GS bytes (16-B multiple), LDS rows GSL = GS + 4 bytes
+// (an odd number of dwords, so lane-private rows sit on distinct LDS banks).
+__device__ __forceinline__ void grid_copy_in(uint8_t *lds, const uint8_t *g, int ne, int GS, int GSL) {
+    const int q = GS >> 4;                              // 16-B chunks per row
     const uint4 *src = reinterpret_cast<const uint4 *>(g);
-    uint4 *dst = reinterpret_cast<uint4 *>(lds);
-    for (int i = threadIdx.x; i < n16; i += BLOCK_THREADS) dst[i] = src[i];
-    for (int i = (n16 << 4) + threadIdx.x; i < nbytes; i += BLOCK_THREADS) lds[i] = g[i];
+    for (int i = threadIdx.x; i < ne * q; i += BLOCK_THREADS) {
+        const int e = i / q, c = i - e * q;
+        const uint4 v = src[i];
+        uint32_t *d = reinterpret_cast<uint32_t *>(lds + e * GSL + c * 16);
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+}
+__device__ __forceinline__ void grid_copy_out(uint8_t *g, const uint8_t *lds, int ne, int GS, int GSL,
+                                              const uint8_t *dirty /* null = all */) {
+    const int q = GS >> 4;
+    uint4 *dst = reinterpret_cast<uint4 *>(g);
+    for (int i = threadIdx.x; i < ne * q; i += BLOCK_THREADS) {
+        const int e = i / q, c = i - e * q;
+        if (dirty && !dirty[e]) continue;
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(lds + e * GSL + c * 16);
+        dst[i] = make_uint4(s[0], s[1], s[2], s[3]);
+    }
 }
 
 // Mission-stack slot writer: slot `s` of env row gets mission tokens or zeros.
 __device__ __forceinline__ void write_mission_slot(void *mis, int mission64, int64_t e, int n_stack, int s,
                                                    const uint8_t *tok /* null = zeros */) {
+    uint4 t0 = make_uint4(0, 0, 0, 0), t1 = t0;
+    if (tok) {
+        t0 = reinterpret_cast<const uint4 *>(tok)[0];
+        t1 = reinterpret_cast<const uint4 *>(tok)[1];
+    }
     if (mission64) {
-        int64_t *row = reinterpret_cast<int64_t *>(mis) + (e * n_stack + s) * 32;
-        longlong2 *r2 = reinterpret_cast<longlong2 *>(row);
+        longlong2 *r2 = reinterpret_cast<longlong2 *>(reinterpret_cast<int64_t *>(mis) + (e * n_stack + s) * 32);
+        const uint32_t w[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
 #pragma unroll
         for (int k = 0; k < 16; k++) {
+            const uint32_t word = w[k >> 1];
+            const int sh = (k & 1) * 16;
             longlong2 v;
-            v.x = tok ? (long long)tok[2 * k] : 0;
-            v.y = tok ? (long long)tok[2 * k + 1] : 0;
+            v.x = (long long)((word >> sh) & 0xFF);
+            v.y = (long long)((word >> (sh + 8)) & 0xFF);
             r2[k] = v;
         }
     } else {
         uint4 *row = reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(mis) + (e * n_stack + s) * 32);
-        uint4 z = make_uint4(0, 0, 0, 0);
-        row[0] = tok ? reinterpret_cast<const uint4 *>(tok)[0] : z;
-        row[1] = tok ? reinterpret_cast<const uint4 *>(tok)[1] : z;
+        row[0] = t0;
+        row[1] = t1;
     }
 }
 
@@ -110,9 +132,7 @@ __device__ __forceinline__ void dir_stack_roll(const uint8_t *src, uint8_t *dst,
         uint4 o = make_uint4(v.y, v.z, v.w, oh);
         reinterpret_cast<uint4 *>(dst)[e] = o;
     } else {
-        uint8_t tmp[32];
-        for (int k = 0; k < nb - 4; k++) tmp[k] = src[e * nb + 4 + k];
-        for (int k = 0; k < nb - 4; k++) dst[e * nb + k] = tmp[k];
+        for (int k = 0; k < nb - 4; k++) dst[e * nb + k] = src[e * nb + 4 + k];   // forward: safe in place
         for (int k = 0; k < 4; k++) dst[e * nb + nb - 4 + k] = (uint8_t)(k == newdir);
     }
 }
@@ -131,7 +151,7 @@ __device__ __forceinline__ void load_gen(Gen &G, const KParams &p, int64_t e, ui
     G.table = p.mt;
     G.tlen = p.tlen;
     G.win = reinterpret_cast<uint32_t *>(scratch + lane * (WIN_STRIDE * 4));
-    G.objs = reinterpret_cast<uint32_t *>(scratch + BLOCK_ENVS * (WIN_STRIDE * 4) + lane * (MAX_OBJS * 4));
+    G.objs = reinterpret_cast<uint32_t *>(scratch + BLOCK_ENVS * (WIN_STRIDE * 4) + lane * (OBJ_STRIDE * 4));
     G.llw = p.llw;
     G.err = 0;
     G.problem = p.problem;
@@ -188,7 +208,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
     if (tid < ne) {
         const int64_t e = e0 + tid;
         Gen G;
-        load_gen(G, p, e, s_grid + tid * p.GS, s_scr, tid);
+        load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
         pcg_seed(G.pcg, (uint64_t)(p.seed_base + e));   // gymnasium Env.reset(seed=seed+i)
         G.cur = 0;                                       // random.seed(cfg.seed) in every worker
         G.wbase = ~0ull >> 1;
@@ -213,13 +233,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
         if (G.err) atomicOr(&s_err, G.err);
     }
     __syncthreads();
-    // grid write-back
-    {
-        const int nbytes = ne * p.GS;
-        uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * p.GS);
-        const uint4 *src = reinterpret_cast<const uint4 *>(s_grid);
-        for (int i = tid; i < (nbytes >> 4); i += BLOCK_THREADS) dst[i] = src[i];
-    }
+    grid_copy_out(p.grid + e0 * p.GS, s_grid, ne, p.GS, p.GSL, nullptr);
     if (tid == 0) {
         atomicAdd(&p.counters[1], (unsigned long long)ne);
         atomicAdd(&p.counters[2], s_ll);
@@ -233,7 +247,7 @@ template <typename ActT>
 __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut o, const ActT *__restrict__ actions) {
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t *s_stk = smem;                       // image stacks [64][img_bytes]; later reset scratch
-    uint8_t *s_grid = smem + p.stk_lds;          // grids [64][GS]
+    uint8_t *s_grid = smem + p.stk_lds;          // grids [64][GSL]
     __shared__ uint8_t s_done[BLOCK_ENVS];
     __shared__ uint8_t s_dirty[BLOCK_ENVS];
     __shared__ uint8_t s_term_out[BLOCK_ENVS];   // write terminal image stack
@@ -245,9 +259,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     const int ne = (int)min<int64_t>(BLOCK_ENVS, p.n - e0);
     const int IMG = p.img_bytes;
     if (tid == 0) { s_ndone = 0; s_ll = 0; s_maxcur = 0; s_err = 0; }
+#ifdef MGX_STAMPS
+    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+    unsigned long long ts1 = 0, ts2 = 0, ts3 = 0;
+#endif
 
     // ---- phase 1: stage grids + image stacks (slot 0 of each env is dead: skip it)
-    coop_copy_in(s_grid, p.grid + e0 * p.GS, ne * p.GS);
+    grid_copy_in(s_grid, p.grid + e0 * p.GS, ne, p.GS, p.GSL);
     {
         const uint8_t *gimg = o.img + e0 * (int64_t)IMG;
         const int nbytes = ne * IMG;
@@ -274,7 +292,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         st = p.state[e];
         int a = (int)actions[e];
         if ((unsigned)a > 6u) { my_err |= MGX_DEVERR_BAD_ACTION; a = -1; }
-        uint8_t *g = s_grid + tid * p.GS;
+        uint8_t *g = s_grid + tid * p.GSL;
         const int S = p.S, ms = S * S;
         const int sc = st.step_count + 1;
         int ax = st.ax, ay = st.ay, dir = st.dir;
@@ -389,36 +407,38 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         s_done[tid] = 0; s_dirty[tid] = 0; s_term_out[tid] = 0;
     }
     __syncthreads();
+#ifdef MGX_STAMPS
+    ts1 = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- phase 3: write the rolled image stacks (newest frame sits in slot 0 of LDS)
     {
         uint8_t *gimg = o.img + e0 * (int64_t)IMG;
-        const int nbytes = ne * IMG;
-        const int n16 = nbytes >> 4;
-        for (int i = tid; i < n16; i += BLOCK_THREADS) {
-            int b = i << 4;
-            int e = b / IMG, off = b - e * IMG;
-            uint32_t w[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                uint32_t acc = 0;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    int src = off + FRAME;
-                    if (src >= IMG) src -= IMG;
-                    uint32_t v = s_done[e] ? 0u : s_stk[e * IMG + src];
-                    acc |= v << (8 * r);
-                    if (++off == IMG) { off = 0; e++; }
+        if ((IMG & 3) == 0) {
+            // dword path (n_stack % 4 == 0): out byte o = lds[(o + 147) mod IMG]
+            //   -> out dword j = alignbyte(dw[(j+37) mod DW], dw[(j+36) mod DW], 3)
+            const int DW = IMG >> 2;
+            const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s_stk);
+            uint32_t *g32 = reinterpret_cast<uint32_t *>(gimg);
+            for (int k = tid; k < ne * DW; k += BLOCK_THREADS) {
+                const int e = k / DW, j = k - e * DW;
+                uint32_t out = 0;
+                if (!s_done[e]) {
+                    int j0 = j + FRAME / 4;
+                    if (j0 >= DW) j0 -= DW;
+                    const int j1 = (j0 + 1 == DW) ? 0 : j0 + 1;
+                    out = __builtin_amdgcn_alignbyte(s32[e * DW + j1], s32[e * DW + j0], FRAME & 3);
                 }
-                w[q] = acc;
+                g32[k] = out;
             }
-            reinterpret_cast<uint4 *>(gimg)[i] = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-        for (int b = (n16 << 4) + tid; b < nbytes; b += BLOCK_THREADS) {
-            int e = b / IMG, off = b - e * IMG;
-            int src = off + FRAME;
-            if (src >= IMG) src -= IMG;
-            gimg[b] = s_done[e] ? 0 : s_stk[e * IMG + src];
+        } else {
+            const int nbytes = ne * IMG;
+            for (int b = tid; b < nbytes; b += BLOCK_THREADS) {
+                const int e = b / IMG, off = b - e * IMG;
+                int src = off + FRAME;
+                if (src >= IMG) src -= IMG;
+                gimg[b] = s_done[e] ? 0 : s_stk[e * IMG + src];
+            }
         }
         // terminal stacks (rare: done envs that asked for one)
         if (p.terminal_mode != MGX_TERMINAL_NONE && s_ndone) {
@@ -434,13 +454,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         }
     }
     __syncthreads();
+#ifdef MGX_STAMPS
+    ts2 = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- phase 4: fused auto-reset of done envs (SubprocVecEnv: env.reset() unseeded)
     if (s_ndone) {
         if (tid < ne && done) {
             const int64_t e = e0 + tid;
             Gen G;
-            load_gen(G, p, e, s_grid + tid * p.GS, s_stk, tid);
+            load_gen(G, p, e, s_grid + tid * p.GSL, s_stk, tid);
             load_rng(G, p, e);
             ResetOut R;
             reset_env(G, R);
@@ -463,15 +486,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         __syncthreads();
     }
     if (my_err) atomicOr(&s_err, my_err);
+#ifdef MGX_STAMPS
+    ts3 = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- phase 5: write back grids that changed
-    {
-        const int per = p.GS >> 4;
-        uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * p.GS);
-        const uint4 *src = reinterpret_cast<const uint4 *>(s_grid);
-        for (int i = tid; i < ne * per; i += BLOCK_THREADS)
-            if (s_dirty[i / per]) dst[i] = src[i];
-    }
+    grid_copy_out(p.grid + e0 * p.GS, s_grid, ne, p.GS, p.GSL, s_dirty);
     __syncthreads();
     if (tid == 0) {
         atomicAdd(&p.counters[0], (unsigned long long)ne);
@@ -481,6 +501,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
             atomicMax(&p.counters[3], s_maxcur);
         }
         if (s_err) atomicOr(p.err, s_err);
+#ifdef MGX_STAMPS
+        const unsigned long long ts4 = __builtin_amdgcn_s_memtime();
+        atomicAdd(&p.counters[4], ts1 - ts0);   // phase 1+2: stage + step logic
+        atomicAdd(&p.counters[5], ts2 - ts1);   // phase 3: stack roll write-back
+        atomicAdd(&p.counters[6], ts3 - ts2);   // phase 4: fused resets
+        atomicAdd(&p.counters[7], ts4 - ts3);   // phase 5: grid write-back
+#endif
     }
 }
 
@@ -756,6 +783,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.seed_base = cfg->base_seed + cfg->env_index_offset;
     p.S = S;
     p.GS = GS;
+    p.GSL = GS + 4;
     p.n_stack = cfg->n_stack;
     p.img_bytes = IMG;
     const int scratch = BLOCK_ENVS * SCRATCH_PER_ENV;
@@ -767,7 +795,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.llw = (uint32_t)h->cfg.livelock_words;
     p.terminal_mode = cfg->terminal_mode;
     p.mission64 = cfg->mission_int64;
-    h->lds_step = (size_t)p.stk_lds + (size_t)BLOCK_ENVS * GS;
+    h->lds_step = (size_t)p.stk_lds + (size_t)BLOCK_ENVS * (GS + 4);
     h->lds_reset = h->lds_step;
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
@@ -871,9 +899,9 @@ mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits) {
 mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[4]) {
     if (!h || !out) return fail(MGX_ERR_INVALID, "null argument");
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    unsigned long long c[4];
+    unsigned long long c[8];
     HIP_TRY(hipMemcpy(c, h->kp.counters, sizeof c, hipMemcpyDeviceToHost));
-    for (int i = 0; i < 4; i++) out[i] = c[i];
+    for (int i = 0; i < 8; i++) out[i] = c[i];
     return MGX_OK;
 }
 

@@ -119,9 +119,10 @@ class MgxEngine:
             raise _lib.MgxError("device error: " + "; ".join(msgs))
 
     def stats(self):
-        out = (ctypes.c_uint64 * 4)()
+        out = (ctypes.c_uint64 * 8)()
         _lib.check(self.L.mgx_stats(self.h, self._stream(), out), "mgx_stats")
-        return dict(steps=int(out[0]), resets=int(out[1]), livelocks=int(out[2]), max_mt_cursor=int(out[3]))
+        return dict(steps=int(out[0]), resets=int(out[1]), livelocks=int(out[2]), max_mt_cursor=int(out[3]),
+                    phase_clocks=[int(out[i]) for i in range(4, 8)])
 
     def dump_state(self):
         import numpy as np
