@@ -82,6 +82,8 @@ typedef struct mgx_config {
     int32_t mission_int64;     /* 1: mission tokens int64 (TokenizeVocabWrapper dtype), 0: uint8 */
     int32_t reserved;
     int64_t mt_table_words;    /* 0 -> default (2^24); shared MT19937 output table length */
+    int32_t ring_depth;        /* pre-generated episodes per env (0 -> 64, max 255; -1 = no ring, inline resets) */
+    int32_t refill_every;      /* steps between ring refills (0 -> ring_depth; <= ring_depth) */
 } mgx_config;
 
 /* Stacked observation in the layout SB3's VecFrameStack(VecTransposeImage(.))
@@ -119,7 +121,9 @@ mgx_status mgx_destroy(mgx_handle *h);
  * (zeros + newest frame).  `livelock_dev` (optional i32 [N]). */
 mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, void *stream);
 
-/* One vectorised step.  actions_dev: [N] int32 (action_bytes = 4) or int64 (8). */
+/* One vectorised step.  actions_dev: [N] int32 (action_bytes = 4) or int64 (8).
+ * Every `refill_every` calls it also enqueues the ring refill (episode
+ * pre-generation); the launch sequence depends only on the call count. */
 mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes,
                     const mgx_step_out *out, void *stream);
 

@@ -201,6 +201,11 @@ __device__ __forceinline__ void pcg_seed(Pcg &p, uint64_t seed) {
 }
 
 // ------------------------------------------------------------ generator context
+// Generation is one long serial RNG chain per env, so its cost is latency: the
+// generator therefore keeps everything it tests in registers -- occupancy and
+// door-adjacency as S*S-bit masks (NW 64-bit words), the next four MT19937
+// words in a register queue -- and only WRITES the cell codes to the LDS grid
+// row (read back once, when the finished grid is copied out).
 constexpr int MT_WIN = 64;        // words per lane-private LDS window
 constexpr int WIN_STRIDE = 65;    // words per lane window (odd -> lane-private rows hit distinct banks)
 constexpr int MAX_OBJS = 32;
@@ -208,14 +213,54 @@ constexpr int OBJ_STRIDE = 33;    // words per lane objs list (odd, same reason)
 constexpr int SAT_PROBE = 64;     // rejections before the exhaustive satisfiability probe
 constexpr uint32_t PCG_LOOP_LIMIT = 1u << 20;
 
+template <int NW>
+struct Bits {                     // S*S-bit set, bit b = y*S + x; named words (no array: stays in VGPRs)
+    uint64_t w0, w1, w2, w3;
+    __device__ __forceinline__ void clear() { w0 = w1 = w2 = w3 = 0; }
+    __device__ __forceinline__ bool test(int b) const {
+        const int i = b >> 6;
+        uint64_t v = w0;
+        if (NW > 1) v = i == 1 ? w1 : v;
+        if (NW > 2) { v = i == 2 ? w2 : v; v = i == 3 ? w3 : v; }
+        return (v >> (b & 63)) & 1ull;
+    }
+    __device__ __forceinline__ void set(int b) {
+        const int i = b >> 6;
+        const uint64_t m = 1ull << (b & 63);
+        w0 |= i == 0 ? m : 0ull;
+        if (NW > 1) w1 |= i == 1 ? m : 0ull;
+        if (NW > 2) { w2 |= i == 2 ? m : 0ull; w3 |= i == 3 ? m : 0ull; }
+    }
+    __device__ __forceinline__ void unset(int b) {
+        const int i = b >> 6;
+        const uint64_t m = ~(1ull << (b & 63));
+        w0 &= i == 0 ? m : ~0ull;
+        if (NW > 1) w1 &= i == 1 ? m : ~0ull;
+        if (NW > 2) { w2 &= i == 2 ? m : ~0ull; w3 &= i == 3 ? m : ~0ull; }
+    }
+};
+
+// S > 11 (four 64-bit words): a register mask set makes the generator state too
+// large to stay in VGPRs; there the generator reads its LDS grid row instead.
+template <>
+struct Bits<4> {
+    __device__ __forceinline__ void clear() {}
+    __device__ __forceinline__ void set(int) {}
+    __device__ __forceinline__ void unset(int) {}
+};
+
+template <int NW>
 struct Gen {
-    uint8_t *g;            // LDS grid slot (S*S used, row-major y*S+x)
+    uint8_t *g;            // LDS grid row (S*S used, row-major y*S+x), write-mostly
     int S;
-    // MT19937 shared table + cursor
+    Bits<NW> occ;          // cell holds an object (walls, doors, goal, keys, boxes, balls)
+    Bits<NW> dn;           // cell is next to a door (custom_env.py:2036-2046)
+    // MT19937 shared table + cursor: q0..q3 = table[cur .. cur+3]
     const uint32_t *table;
     uint64_t tlen;
-    uint32_t *win;         // LDS window (MT_WIN words, 16-B aligned)
+    uint32_t *win;         // LDS window (MT_WIN words) = table[wbase .. wbase + MT_WIN)
     uint64_t wbase, cur, astart;
+    uint32_t q0, q1, q2, q3;
     uint32_t llw;
     bool abort;
     uint32_t err;
@@ -227,92 +272,139 @@ struct Gen {
     int problem, cfg_mission, num_objects, all_doors_open;
 };
 
-__device__ __forceinline__ uint8_t &cell(Gen &G, int x, int y) { return G.g[y * G.S + x]; }
+template <int NW>
+__device__ __forceinline__ void put(Gen<NW> &G, int x, int y, uint8_t code) {   // grid.set(x, y, obj)
+    const int b = y * G.S + x;
+    G.g[b] = code;
+    if (code == CODE_EMPTY) G.occ.unset(b); else G.occ.set(b);
+}
 
-// Refill the lane's LDS window with table[cur & ~3 .. +MT_WIN): 16 independent
+// Refill the lane's LDS window with table[from & ~3 .. +MT_WIN): 16 independent
 // 16-B global loads in flight (one L2/HBM round trip), 64 dword LDS stores
 // (the window row is 4-B aligned: odd dword stride avoids bank conflicts).
 __device__ __forceinline__ uint64_t mt_refill(const uint32_t *__restrict__ table, uint64_t tlen, uint32_t *win,
-                                              uint64_t cur, uint32_t &err) {
-    uint64_t base = cur & ~3ull;
+                                              uint64_t from, uint32_t &err) {
+    uint64_t base = from & ~3ull;
     if (base + MT_WIN > tlen) { err |= 1u; base = tlen; }   // MGX_DEVERR_MT_TABLE: read the zero pad
     const uint4 *src = reinterpret_cast<const uint4 *>(table + base);
-    uint4 v[MT_WIN / 4];
 #pragma unroll
-    for (int k = 0; k < MT_WIN / 4; k++) v[k] = src[k];
-#pragma unroll
-    for (int k = 0; k < MT_WIN / 4; k++) {
-        win[4 * k] = v[k].x; win[4 * k + 1] = v[k].y; win[4 * k + 2] = v[k].z; win[4 * k + 3] = v[k].w;
+    for (int h = 0; h < MT_WIN / 16; h++) {        // 4 x (4 loads in flight, then 16 LDS stores)
+        uint4 v0 = src[4 * h], v1 = src[4 * h + 1], v2 = src[4 * h + 2], v3 = src[4 * h + 3];
+        uint32_t *d = win + 16 * h;
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
+        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
+        d[8] = v2.x; d[9] = v2.y; d[10] = v2.z; d[11] = v2.w;
+        d[12] = v3.x; d[13] = v3.y; d[14] = v3.z; d[15] = v3.w;
     }
     return base;
 }
 
-__device__ __forceinline__ uint32_t mt_word(Gen &G) {
-    if (G.cur - G.astart >= G.llw) { G.abort = true; return 0; }
-    uint64_t off = G.cur - G.wbase;
+template <int NW>
+__device__ __forceinline__ uint32_t win_word(Gen<NW> &G, uint64_t idx) {
+    uint64_t off = idx - G.wbase;
     if (off >= MT_WIN) {
-        G.wbase = mt_refill(G.table, G.tlen, G.win, G.cur, G.err);
-        off = G.cur - G.wbase;
+        G.wbase = mt_refill(G.table, G.tlen, G.win, idx, G.err);
+        off = idx - G.wbase;
         if (off >= MT_WIN) off = 0;   // only after MGX_DEVERR_MT_TABLE
     }
-    G.cur++;
     return G.win[off];
 }
+// (re)load the register queue at the current cursor
+template <int NW>
+__device__ __forceinline__ void mt_sync(Gen<NW> &G) {
+    G.q0 = win_word(G, G.cur);
+    G.q1 = win_word(G, G.cur + 1);
+    G.q2 = win_word(G, G.cur + 2);
+    G.q3 = win_word(G, G.cur + 3);
+}
+// getrandbits(32): the next MT19937 word of this env's stream (live-lock capped)
+template <int NW>
+__device__ __forceinline__ uint32_t mt_word(Gen<NW> &G) {
+    if (G.cur - G.astart >= G.llw) { G.abort = true; return 0; }
+    const uint32_t w = G.q0;
+    G.q0 = G.q1; G.q1 = G.q2; G.q2 = G.q3;
+    G.q3 = win_word(G, G.cur + 4);      // LDS read issued four draws before it is needed
+    G.cur++;
+    return w;
+}
 // random._randbelow_with_getrandbits(n), n >= 1
-__device__ __forceinline__ int randbelow(Gen &G, uint32_t n) {
-    int k = 32 - __clz(n);
+template <int NW>
+__device__ __forceinline__ int randbelow(Gen<NW> &G, uint32_t n) {
+    const int k = 32 - __clz(n);
     for (;;) {
-        uint32_t w = mt_word(G);
+        const uint32_t w = mt_word(G);
         if (G.abort) return 0;
-        uint32_t r = k == 32 ? w : (w >> (32 - k));
+        const uint32_t r = k == 32 ? w : (w >> (32 - k));
         if (r < n) return (int)r;
     }
 }
-__device__ __forceinline__ int randint(Gen &G, int a, int b) { return a + randbelow(G, (uint32_t)(b - a + 1)); }
-__device__ __forceinline__ bool choice_bool(Gen &G) { return randbelow(G, 2) == 0; }   // choice([True, False])
+template <int NW>
+__device__ __forceinline__ int randint(Gen<NW> &G, int a, int b) { return a + randbelow(G, (uint32_t)(b - a + 1)); }
+template <int NW>
+__device__ __forceinline__ bool choice_bool(Gen<NW> &G) { return randbelow(G, 2) == 0; }   // choice([True, False])
 
-__device__ __forceinline__ bool next2door(Gen &G, int x, int y) {
-    return is_door(cell(G, x - 1, y)) || is_door(cell(G, x + 1, y)) ||
-           is_door(cell(G, x, y - 1)) || is_door(cell(G, x, y + 1));
+template <int NW>
+__device__ __forceinline__ bool next2door(const Gen<NW> &G, int x, int y) {
+    if constexpr (NW == 4) {
+        return is_door(G.g[y * G.S + x - 1]) || is_door(G.g[y * G.S + x + 1]) ||
+               is_door(G.g[(y - 1) * G.S + x]) || is_door(G.g[(y + 1) * G.S + x]);
+    } else {
+        return G.dn.test(y * G.S + x);
+    }
+}
+template <int NW>
+__device__ __forceinline__ bool occupied(const Gen<NW> &G, int b) {
+    if constexpr (NW == 4) return G.g[b] != CODE_EMPTY;
+    else return G.occ.test(b);
 }
 
-__device__ __forceinline__ void add_obj(Gen &G, int t, int cname, int x, int y) {
+template <int NW>
+__device__ __forceinline__ void add_obj(Gen<NW> &G, int t, int cname, int x, int y) {
     if (G.nobjs >= MAX_OBJS) { G.err |= 8u; return; }
     G.objs[G.nobjs++] = (uint32_t)t | ((uint32_t)(cname & 15) << 4) | ((uint32_t)x << 8) | ((uint32_t)y << 16);
 }
 
-// MiniGridEnv.place_obj(obj) over the whole grid (PCG64)
-__device__ __forceinline__ void place_obj_any(Gen &G, uint8_t code, int &px, int &py) {
+// MiniGridEnv.place_obj position draw over the whole grid (PCG64): rejects occupied
+// cells and the agent's cell; `commit` decides what (if anything) lands there.
+template <int NW>
+__device__ __forceinline__ void draw_free_cell(Gen<NW> &G, int &px, int &py) {
     for (uint32_t it = 0;; ++it) {
         if (it > PCG_LOOP_LIMIT) { G.err |= 4u; px = 1; py = 1; return; }
-        int x = pcg_integers(G.pcg, 0, G.S);
-        int y = pcg_integers(G.pcg, 0, G.S);
-        if (cell(G, x, y) != CODE_EMPTY) continue;
+        const int x = pcg_integers(G.pcg, 0, G.S);
+        const int y = pcg_integers(G.pcg, 0, G.S);
+        if (occupied(G, y * G.S + x)) continue;
         if (x == G.ax && y == G.ay) continue;
-        cell(G, x, y) = code;
         px = x; py = y;
         return;
     }
 }
-__device__ __forceinline__ void place_agent(Gen &G) {
+template <int NW>
+__device__ __forceinline__ void place_agent(Gen<NW> &G) {        // place_obj(None) + random dir
     G.ax = -1; G.ay = -1;
     int x, y;
-    place_obj_any(G, CODE_EMPTY, x, y);
+    draw_free_cell(G, x, y);
     G.ax = x; G.ay = y;
     G.adir = pcg_integers(G.pcg, 0, 4);
 }
 
 // ---- ordered choice lists as bitmasks (list.remove keeps order) --------------
 // element b of an obj_choice list = (types[b / 6], COLOR_NAMES[b % 6])
-__device__ __forceinline__ int nth_set_bit(uint32_t m, int r) {
-    for (int i = 0; i < r; i++) m &= m - 1;
-    return __ffs(m) - 1;
+__device__ __forceinline__ int nth_set_bit(uint32_t m, int r) {   // branchless rank-select, r < popc(m)
+    int pos = 0, c;
+    c = __popc(m & 0xFFFFu); if (r >= c) { r -= c; m >>= 16; pos += 16; }
+    c = __popc(m & 0xFFu);   if (r >= c) { r -= c; m >>= 8;  pos += 8; }
+    c = __popc(m & 0xFu);    if (r >= c) { r -= c; m >>= 4;  pos += 4; }
+    c = __popc(m & 0x3u);    if (r >= c) { r -= c; m >>= 2;  pos += 2; }
+    c = (int)(m & 1u);       if (r >= c) { pos += 1; }
+    return pos;
 }
-__device__ __forceinline__ int mask_choice(Gen &G, uint32_t m) {   // index into the list
+template <int NW>
+__device__ __forceinline__ int mask_choice(Gen<NW> &G, uint32_t m) {   // index into the list
     return nth_set_bit(m, randbelow(G, (uint32_t)__popc(m)));
 }
 
-__device__ __forceinline__ void live_lock(Gen &G) {
+template <int NW>
+__device__ __forceinline__ void live_lock(Gen<NW> &G) {
     // provably unsatisfiable `while True` loop: the reference would spin until the
     // cap; that consumes exactly llw words of this attempt -- jump there.
     G.cur = G.astart + G.llw;
@@ -321,15 +413,16 @@ __device__ __forceinline__ void live_lock(Gen &G) {
 
 // `while True: p=(randint(x0,x1), randint(y0,y1)); if p!=goal and [p!=agent] and
 //  [p!=other] and not next2door(p): break` -> grid.set(Box(c,Key(c)) | Key(c)); objs.append
-__device__ __forceinline__ void place_key(Gen &G, int x0, int x1, int y0, int y1, int gx, int gy, bool chk_agent,
-                                 int ox, int oy, int cname, bool kib, int *kx, int *ky) {
+template <int NW>
+__device__ __forceinline__ void place_key(Gen<NW> &G, int x0, int x1, int y0, int y1, int gx, int gy, bool chk_agent,
+                                          int ox, int oy, int cname, bool kib, int *kx, int *ky) {
     int x, y, rej = 0;
     for (;;) {
         x = randint(G, x0, x1);
         y = randint(G, y0, y1);
         if (G.abort) return;
-        bool bad = (x == gx && y == gy) || (chk_agent && x == G.ax && y == G.ay) || (x == ox && y == oy) ||
-                   next2door(G, x, y);
+        const bool bad = (x == gx && y == gy) || (chk_agent && x == G.ax && y == G.ay) || (x == ox && y == oy) ||
+                         next2door(G, x, y);
         if (!bad) break;
         if (++rej == SAT_PROBE) {
             bool sat = false;
@@ -340,55 +433,69 @@ __device__ __forceinline__ void place_key(Gen &G, int x0, int x1, int y0, int y1
             if (!sat) { live_lock(G); return; }
         }
     }
-    int cidx = cn2idx(cname);
-    if (kib) { cell(G, x, y) = mk_code(T_BOX, cidx, 1); add_obj(G, T_BOX, cname, x, y); }
-    else { cell(G, x, y) = mk_code(T_KEY, cidx, 0); add_obj(G, T_KEY, cname, x, y); }
+    const int cidx = cn2idx(cname);
+    if (kib) { put(G, x, y, mk_code(T_BOX, cidx, 1)); add_obj(G, T_BOX, cname, x, y); }
+    else { put(G, x, y, mk_code(T_KEY, cidx, 0)); add_obj(G, T_KEY, cname, x, y); }
     if (kx) { *kx = x; *ky = y; }
 }
 
 // `for _ in range(n): (t,c)=choice(obj_choice); obj_choice.remove((t,c)); while True:
 //  p=(randint..); [p in objs -> retry]; if p != agent and not next2door(p): break; put_obj`
-// (p in objs <=> grid cell occupied, inside a room interior)
-__device__ __forceinline__ void place_objects(Gen &G, uint32_t &oc, const int *types, int n, int x0, int x1,
-                                     int y0, int y1) {
+// (p in objs <=> cell occupied, inside a room interior)
+template <int NW>
+__device__ __forceinline__ void place_objects(Gen<NW> &G, uint32_t &oc, const int *types, int n, int x0, int x1,
+                                              int y0, int y1) {
     for (int k = 0; k < n; k++) {
         if (oc == 0) { G.err |= 8u; return; }
-        int b = mask_choice(G, oc);
+        const int b = mask_choice(G, oc);
         if (G.abort) return;
         oc &= ~(1u << b);
-        int t = types[b / 6], cname = b % 6;
+        const int t = types[b / 6], cname = b % 6;
         int x, y, rej = 0;
         for (;;) {
             x = randint(G, x0, x1);
             y = randint(G, y0, y1);
             if (G.abort) return;
-            bool bad = cell(G, x, y) != CODE_EMPTY || (x == G.ax && y == G.ay) || next2door(G, x, y);
+            const bool bad = occupied(G, y * G.S + x) || (x == G.ax && y == G.ay) || next2door(G, x, y);
             if (!bad) break;
             if (++rej == SAT_PROBE) {
                 bool sat = false;
                 for (int xx = x0; xx <= x1 && !sat; xx++)
                     for (int yy = y0; yy <= y1 && !sat; yy++)
-                        sat = !(cell(G, xx, yy) != CODE_EMPTY || (xx == G.ax && yy == G.ay) || next2door(G, xx, yy));
+                        sat = !(occupied(G, yy * G.S + xx) || (xx == G.ax && yy == G.ay) || next2door(G, xx, yy));
                 if (!sat) { live_lock(G); return; }
             }
         }
-        cell(G, x, y) = mk_code(t, cn2idx(cname), 0);
+        put(G, x, y, mk_code(t, cn2idx(cname), 0));
         add_obj(G, t, cname, x, y);
     }
 }
 
-__device__ __forceinline__ void place_goal_multi(Gen &G, int &gx, int &gy) {
+// `while True: goal_pos = place_obj(Goal()); if next2door: grid.set(None); continue`
+template <int NW>
+__device__ __forceinline__ void place_goal_multi(Gen<NW> &G, int &gx, int &gy) {
     for (uint32_t it = 0;; ++it) {
         if (it > PCG_LOOP_LIMIT) { G.err |= 4u; break; }
-        place_obj_any(G, CODE_GOAL, gx, gy);
-        if (next2door(G, gx, gy)) { cell(G, gx, gy) = CODE_EMPTY; continue; }
+        draw_free_cell(G, gx, gy);
+        if (next2door(G, gx, gy)) continue;      // placed then removed: net no-op
         break;
     }
+    put(G, gx, gy, CODE_GOAL);
     add_obj(G, T_GOAL, 15, gx, gy);
 }
 
 __device__ __forceinline__ int door_code(int cname, bool locked, bool open) {
     return open ? mk_code(T_OPEN, cn2idx(cname), 0) : mk_code(T_DOOR, cn2idx(cname), locked ? 1 : 0);
+}
+
+template <int NW>
+__device__ __forceinline__ void put_door(Gen<NW> &G, int x, int y, uint8_t code) {
+    put(G, x, y, code);
+    const int S = G.S, b = y * S + x;
+    if (x > 0) G.dn.set(b - 1);
+    if (x < S - 1) G.dn.set(b + 1);
+    if (y > 0) G.dn.set(b - S);
+    if (y < S - 1) G.dn.set(b + S);
 }
 
 // ---- multi-room layouts, table-driven (custom_env.py:617-2034) ---------------
@@ -400,7 +507,7 @@ __device__ __forceinline__ int door_code(int cname, bool locked, bool open) {
 // Rooms are visited in the reference's order:
 //   2: L, R;  3: UL, LL, R;  4: UL, LL, UR, LR.
 
-// door d of an nr-room layout: bit0 = horizontal (x drawn, y = mid); range lo..hi
+// door d of an nr-room layout: horizontal (x drawn, y = mid) or vertical; range lo..hi
 __device__ __forceinline__ void door_geom(int nr, int d, int mid, int S, bool &horiz, int &lo, int &hi) {
     if (nr == 2) { horiz = false; lo = 1; hi = S - 2; return; }
     if (nr == 3) {
@@ -456,11 +563,12 @@ __device__ __forceinline__ void key_spec(int nr, int r, int ar, int &kA, int &kB
 
 __device__ const int MULTI_TYPES[3] = {T_KEY, T_BALL, T_BOX};
 
-__device__ __forceinline__ void gen_rooms(Gen &G, int nr) {
+template <int NW>
+__device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     const int S = G.S, mid = S / 2;
-    for (int i = 1; i < S - 1; i++) cell(G, mid, i) = CODE_WALL;
-    if (nr == 3) for (int i = 1; i < mid; i++) cell(G, i, mid) = CODE_WALL;
-    if (nr == 4) for (int i = 1; i < S - 1; i++) cell(G, i, mid) = CODE_WALL;
+    for (int i = 1; i < S - 1; i++) put(G, mid, i, CODE_WALL);
+    if (nr == 3) for (int i = 1; i < mid; i++) put(G, i, mid, CODE_WALL);
+    if (nr == 4) for (int i = 1; i < S - 1; i++) put(G, i, mid, CODE_WALL);
     const int ndoors = nr == 2 ? 1 : nr;
     uint32_t oc = 0x3FFFFu;    // obj_choice: bit = type_slot*6 + colour-name (key, ball, box)
     uint32_t dc = 0x3Fu;       // door_colors
@@ -485,7 +593,7 @@ __device__ __forceinline__ void gen_rooms(Gen &G, int nr) {
         const int x = horiz ? v : mid, y = horiz ? mid : v;
         const uint32_t di = dinfo >> (8 * d);
         const bool open = G.all_doors_open ? choice_bool(G) : false;
-        cell(G, x, y) = (uint8_t)door_code(di & 7, (di >> 3) & 1, open);
+        put_door(G, x, y, (uint8_t)door_code(di & 7, (di >> 3) & 1, open));
         add_obj(G, T_DOOR, di & 7, x, y);
     }
     if (G.abort) return;
@@ -517,7 +625,7 @@ __device__ __forceinline__ void gen_rooms(Gen &G, int nr) {
         if (kB >= 0 && ((dinfo >> (8 * kB + 3)) & 1)) {
             const uint32_t di = dinfo >> (8 * kB);
             ndec++;
-            place_key(G, x0, x1, y0, y1, gx, gy, chk, kx, ky, di & 7, (di >> 4) & 1, 0, 0);
+            place_key(G, x0, x1, y0, y1, gx, gy, chk, kx, ky, di & 7, (di >> 4) & 1, (int *)nullptr, (int *)nullptr);
             if (G.abort) return;
         }
         if (gr == r) ndec++;
@@ -531,11 +639,12 @@ __device__ __forceinline__ void gen_rooms(Gen &G, int nr) {
     }
 }
 
-__device__ __forceinline__ int gen_multi(Gen &G) {             // custom_env.py:595-615
+template <int NW>
+__device__ __forceinline__ int gen_multi(Gen<NW> &G) {             // custom_env.py:595-615
     int cmd;
     if (G.cfg_mission >= 0) cmd = G.cfg_mission;
     else {
-        int r = randbelow(G, 4);                                 // choice([0, 1, 2, 5])
+        const int r = randbelow(G, 4);                               // choice([0, 1, 2, 5])
         cmd = r == 3 ? 5 : r;
     }
     if (G.abort) return 0;
@@ -550,7 +659,8 @@ __device__ const int GTG_T[4] = {T_BOX, T_DOOR, T_KEY, T_BALL};
 __device__ const int OPN_T[2] = {T_BOX, T_DOOR};
 __device__ const int PKP_T[3] = {T_KEY, T_BOX, T_BALL};
 
-__device__ __forceinline__ int gen_single(Gen &G) {                     // custom_env.py:371-513
+template <int NW>
+__device__ __forceinline__ int gen_single(Gen<NW> &G) {           // custom_env.py:371-513
     const int *types;
     int ntypes, cmd;
     bool goal = false;
@@ -563,17 +673,19 @@ __device__ __forceinline__ int gen_single(Gen &G) {                     // custo
     uint32_t oc = (1u << (ntypes * 6)) - 1u;
     for (int k = 0; k < G.num_objects; k++) {
         if (oc == 0) { G.err |= 8u; break; }
-        int b = mask_choice(G, oc);
+        const int b = mask_choice(G, oc);
         if (G.abort) return 0;
         oc &= ~(1u << b);
-        int t = types[b / 6], cname = b % 6;
+        const int t = types[b / 6], cname = b % 6;
         int x, y;
-        place_obj_any(G, mk_code(t, cn2idx(cname), 0), x, y);
+        draw_free_cell(G, x, y);
+        put(G, x, y, mk_code(t, cn2idx(cname), 0));
         add_obj(G, t, cname, x, y);
     }
     if (goal) {
         int x, y;
-        place_obj_any(G, CODE_GOAL, x, y);
+        draw_free_cell(G, x, y);
+        put(G, x, y, CODE_GOAL);
         add_obj(G, T_GOAL, 15, x, y);
     }
     place_agent(G);
@@ -585,16 +697,30 @@ struct ResetOut {
     int livelocks;
 };
 
+template <int NW>
+__device__ __forceinline__ void gen_init(Gen<NW> &G) {}
+
 // One attempt of MiniGridEnv.reset -> PlaygroundEnv._gen_grid (custom_env.py:122-267).
-__device__ __forceinline__ void gen_attempt(Gen &G, ResetOut &R) {
+template <int NW>
+__device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
     const int S = G.S;
-    for (int i = 0; i < S * S; i++) G.g[i] = CODE_EMPTY;
-    for (int i = 0; i < S; i++) {                                 // wall_rect(0, 0, W, H)
-        cell(G, i, 0) = CODE_WALL; cell(G, i, S - 1) = CODE_WALL;
-        cell(G, 0, i) = CODE_WALL; cell(G, S - 1, i) = CODE_WALL;
+    {   // Grid(W, H) of None + wall_rect(0, 0, W, H); the row is 4-B aligned in LDS
+        uint32_t *g32 = reinterpret_cast<uint32_t *>(G.g);
+        const int nw = (S * S + 3) >> 2;
+        for (int i = 0; i < nw; i++) g32[i] = 0x01010101u * CODE_EMPTY;
+        for (int i = 0; i < S; i++) {
+            G.g[i] = CODE_WALL; G.g[(S - 1) * S + i] = CODE_WALL;
+            G.g[i * S] = CODE_WALL; G.g[i * S + S - 1] = CODE_WALL;
+        }
     }
+    G.occ.clear();                                                // wall_rect(0, 0, W, H)
+    for (int i = 0; i < S; i++) {
+        G.occ.set(i); G.occ.set((S - 1) * S + i);
+        G.occ.set(i * S); G.occ.set(i * S + S - 1);
+    }
+    G.dn.clear();
     G.ax = -1; G.ay = -1; G.adir = 0; G.nobjs = 0;
-    int cmd = G.problem == 0 ? gen_multi(G) : gen_single(G);
+    const int cmd = G.problem == 0 ? gen_multi(G) : gen_single(G);
     if (G.abort) return;
     if (cmd == 0) {                                               // 'go to' (np_random.integers)
         int i = 0;
@@ -603,7 +729,7 @@ __device__ __forceinline__ void gen_attempt(Gen &G, ResetOut &R) {
             i = pcg_integers(G.pcg, 0, G.nobjs);
             if ((G.objs[i] & 15) != T_GOAL) break;
         }
-        uint32_t o = G.objs[i];
+        const uint32_t o = G.objs[i];
         R.tx = (uint8_t)(o >> 8); R.ty = (uint8_t)(o >> 16); R.ta = A_DONE;
         R.mission_id = (uint8_t)(CMD_GOTO | (((o >> 4) & 15) << 2) | (type_slot(o & 15) << 5));
     } else if (cmd == 1 || cmd == 2) {                            // 'toggle' / 'pick up' (random.choice)
@@ -611,18 +737,18 @@ __device__ __forceinline__ void gen_attempt(Gen &G, ResetOut &R) {
         for (;;) {
             i = randbelow(G, (uint32_t)G.nobjs);
             if (G.abort) return;
-            int t = G.objs[i] & 15;
+            const int t = G.objs[i] & 15;
             if (cmd == 1 ? (t == T_BOX || t == T_DOOR) : (t == T_BOX || t == T_KEY || t == T_BALL)) break;
             if (++rej == SAT_PROBE) {
                 bool sat = false;
                 for (int k = 0; k < G.nobjs; k++) {
-                    int tk = G.objs[k] & 15;
+                    const int tk = G.objs[k] & 15;
                     sat |= cmd == 1 ? (tk == T_BOX || tk == T_DOOR) : (tk == T_BOX || tk == T_KEY || tk == T_BALL);
                 }
                 if (!sat) { live_lock(G); return; }
             }
         }
-        uint32_t o = G.objs[i];
+        const uint32_t o = G.objs[i];
         R.tx = (uint8_t)(o >> 8); R.ty = (uint8_t)(o >> 16);
         R.ta = cmd == 1 ? A_TOGGLE : A_PICKUP;
         R.mission_id = (uint8_t)((cmd == 1 ? CMD_TOGGLE : CMD_PICKUP) | (((o >> 4) & 15) << 2) |
@@ -637,11 +763,13 @@ __device__ __forceinline__ void gen_attempt(Gen &G, ResetOut &R) {
 }
 
 // MiniGridEnv.reset with the engine's live-lock retry policy.
-__device__ __forceinline__ void reset_env(Gen &G, ResetOut &R) {
+template <int NW>
+__device__ __forceinline__ void reset_env(Gen<NW> &G, ResetOut &R) {
     R.livelocks = 0;
     for (;;) {
         G.astart = G.cur;
         G.abort = false;
+        mt_sync(G);                     // register queue at the attempt's first word
         gen_attempt(G, R);
         if (!G.abort) break;
         R.livelocks++;

@@ -34,6 +34,8 @@ namespace {
 constexpr int BLOCK_ENVS = 64;
 constexpr int BLOCK_THREADS = 256;
 constexpr int FRAME = 147;                 // 3 x 7 x 7
+constexpr int FRAME_DW4 = 147;             // dwords per env row at n_stack == 4 (588 B)
+constexpr int FROW = 148;                  // LDS frame row (fast roll): byte 0 pad, bytes 1..147 frame
 constexpr int SCRATCH_PER_ENV = WIN_STRIDE * 4 + OBJ_STRIDE * 4;   // LDS bytes per resetting lane
 
 struct KParams {
@@ -48,9 +50,21 @@ struct KParams {
     uint64_t tlen;
     int64_t n;
     int64_t seed_base;              // base_seed + env_index_offset
-    int S, GS, GSL, n_stack, img_bytes, stk_lds, problem, cfg_mission, num_objects, all_doors_open;
+    int S, GS, GSL, grid_lds, n_stack, img_bytes, stk_lds, stk_step, problem, cfg_mission, num_objects, all_doors_open;
     uint32_t llw;
-    int terminal_mode, mission64;
+    int terminal_mode, mission64, fast_roll;
+    // pre-generated episode ring (see mgx_refill_kernel)
+    uint8_t *ring_grid;     // [N][D][GS]
+    uint4 *ring_hdr;        // [N][D]   {ax|ay<<8|dir<<16|tx<<24, ty|ta<<8|mission<<16, livelocks, 0}
+    uint4 *ring_rng;        // [N][D][2] RNG snapshot after that episode's generation
+    uint4 *cur_rng;         // [N][2]   RNG snapshot after the current episode's generation
+    uint16_t *ring_ctl;     // [N]      head | count << 8
+    uint32_t *fix_list;     // [N] envs whose ring was empty at their reset (mgx_fixup_kernel)
+    uint32_t *fix_count;    // list length; fix_done: workgroups of the fixup kernel that finished
+    uint32_t *fix_done;
+    ulonglong4 *blk;        // [3 * nblk] per-workgroup stats: step/reset | fixup | refill workgroups
+    int nblk;               // ceil(N / 64)
+    int D;
 };
 
 struct KOut {
@@ -145,13 +159,16 @@ __device__ __forceinline__ void dir_stack_fresh(uint8_t *dst, int64_t e, int n_s
     }
 }
 
-__device__ __forceinline__ void load_gen(Gen &G, const KParams &p, int64_t e, uint8_t *g, uint8_t *scratch, int lane) {
+template <int NW>
+__device__ __forceinline__ void load_gen(Gen<NW> &G, const KParams &p, int64_t e, uint8_t *g, uint8_t *scratch, int lane) {
     G.g = g;
     G.S = p.S;
     G.table = p.mt;
     G.tlen = p.tlen;
-    G.win = reinterpret_cast<uint32_t *>(scratch + lane * (WIN_STRIDE * 4));
-    G.objs = reinterpret_cast<uint32_t *>(scratch + BLOCK_ENVS * (WIN_STRIDE * 4) + lane * (OBJ_STRIDE * 4));
+    // lane >= 0: workgroup LDS layout [64 windows][64 objs lists]; lane < 0: one env's private block
+    G.win = reinterpret_cast<uint32_t *>(scratch + (lane >= 0 ? lane * (WIN_STRIDE * 4) : 0));
+    G.objs = reinterpret_cast<uint32_t *>(scratch + (lane >= 0 ? BLOCK_ENVS * (WIN_STRIDE * 4) + lane * (OBJ_STRIDE * 4)
+                                                               : WIN_STRIDE * 4));
     G.llw = p.llw;
     G.err = 0;
     G.problem = p.problem;
@@ -162,9 +179,11 @@ __device__ __forceinline__ void load_gen(Gen &G, const KParams &p, int64_t e, ui
     G.nobjs = 0;
     G.ax = G.ay = -1;
     G.adir = 0;
+    gen_init(G);
 }
 
-__device__ __forceinline__ void load_rng(Gen &G, const KParams &p, int64_t e) {
+template <int NW>
+__device__ __forceinline__ void load_rng(Gen<NW> &G, const KParams &p, int64_t e) {
     uint4 s = p.pcg[2 * e], i = p.pcg[2 * e + 1], a = p.aux[e];
     G.pcg.sh = ((uint64_t)s.x << 32) | s.y;
     G.pcg.sl = ((uint64_t)s.z << 32) | s.w;
@@ -175,10 +194,23 @@ __device__ __forceinline__ void load_rng(Gen &G, const KParams &p, int64_t e) {
     G.cur = (uint64_t)a.z | ((uint64_t)a.w << 32);
     G.wbase = ~0ull >> 1;   // empty window
 }
-__device__ __forceinline__ void store_rng(const Gen &G, const KParams &p, int64_t e) {
+template <int NW>
+__device__ __forceinline__ void store_rng(const Gen<NW> &G, const KParams &p, int64_t e) {
     p.pcg[2 * e] = make_uint4((uint32_t)(G.pcg.sh >> 32), (uint32_t)G.pcg.sh, (uint32_t)(G.pcg.sl >> 32), (uint32_t)G.pcg.sl);
     p.pcg[2 * e + 1] = make_uint4((uint32_t)(G.pcg.ih >> 32), (uint32_t)G.pcg.ih, (uint32_t)(G.pcg.il >> 32), (uint32_t)G.pcg.il);
     p.aux[e] = make_uint4(G.pcg.uinteger, G.pcg.has, (uint32_t)G.cur, (uint32_t)(G.cur >> 32));
+}
+
+template <int NW>
+__device__ __forceinline__ void rng_snapshot(const Gen<NW> &G, uint4 *dst) {
+    dst[0] = make_uint4((uint32_t)(G.pcg.sh >> 32), (uint32_t)G.pcg.sh, (uint32_t)(G.pcg.sl >> 32), (uint32_t)G.pcg.sl);
+    dst[1] = make_uint4(G.pcg.uinteger, G.pcg.has, (uint32_t)G.cur, (uint32_t)(G.cur >> 32));
+}
+template <int NW>
+__device__ __forceinline__ uint4 pack_hdr(const Gen<NW> &G, const ResetOut &R) {
+    return make_uint4((uint32_t)G.ax | ((uint32_t)G.ay << 8) | ((uint32_t)G.adir << 16) | ((uint32_t)R.tx << 24),
+                      (uint32_t)R.ty | ((uint32_t)R.ta << 8) | ((uint32_t)R.mission_id << 16),
+                      (uint32_t)R.livelocks, 0u);
 }
 
 // Render the first frame of a fresh episode straight into the newest slot of the stack.
@@ -193,6 +225,7 @@ __device__ __forceinline__ void write_fresh_frame(const KParams &p, uint8_t *img
 }
 
 // ============================================================== reset kernel
+template <int NW>
 __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOut o) {
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t *s_scr = smem;
@@ -207,7 +240,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
     __syncthreads();
     if (tid < ne) {
         const int64_t e = e0 + tid;
-        Gen G;
+        Gen<NW> G;
         load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
         pcg_seed(G.pcg, (uint64_t)(p.seed_base + e));   // gymnasium Env.reset(seed=seed+i)
         G.cur = 0;                                       // random.seed(cfg.seed) in every worker
@@ -221,6 +254,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
         st.mission_done = 0; st.frames = 1; st.flags = 0; st.pad = 0;
         p.state[e] = st;
         store_rng(G, p, e);
+        rng_snapshot(G, p.cur_rng + 2 * e);
+        p.ring_ctl[e] = 0;                               // empty ring: filled by mgx_refill_kernel
         // stacked obs: zeros + first frame
         uint8_t *row = o.img + e * (int64_t)p.img_bytes;
         for (int k = 0; k < p.img_bytes - FRAME; k++) row[k] = 0;
@@ -235,73 +270,172 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
     __syncthreads();
     grid_copy_out(p.grid + e0 * p.GS, s_grid, ne, p.GS, p.GSL, nullptr);
     if (tid == 0) {
-        atomicAdd(&p.counters[1], (unsigned long long)ne);
-        atomicAdd(&p.counters[2], s_ll);
-        atomicMax(&p.counters[3], s_maxcur);
+        ulonglong4 b = p.blk[blockIdx.x];           // workgroup-private stats slot (no contention)
+        b.y += (unsigned long long)ne; b.z += s_ll; b.w = b.w > s_maxcur ? b.w : s_maxcur;
+        p.blk[blockIdx.x] = b;
         if (s_err) atomicOr(p.err, s_err);
     }
 }
 
 // =============================================================== step kernel
+// Work split helper: item w -> (list index, cell) with consecutive threads on
+// different envs; one division up front, then incremental.
+struct Split {
+    int li, c, dli, dc, n;
+    __device__ __forceinline__ Split(int w0, int stride, int nlist) : n(nlist) {
+        c = w0 / nlist; li = w0 - c * nlist;
+        dc = stride / nlist; dli = stride - dc * nlist;
+    }
+    __device__ __forceinline__ void next() { li += dli; c += dc; if (li >= n) { li -= n; c++; } }
+};
+
+// Render the 7x7 view of every listed env into its LDS frame row, spreading the
+// (env, cell) pairs over all 256 threads of the workgroup.
+__device__ __forceinline__ void render_block(const uint8_t *s_grid, uint8_t *s_fr, const uint32_t *s_rp,
+                                             const uint8_t *list, int nlist, int S, int GSL, int FSTRIDE,
+                                             int FOFF) {
+    if (nlist == 0) return;
+    const int total = nlist * 49;
+    Split sp(threadIdx.x, BLOCK_THREADS, nlist);
+    for (int w = threadIdx.x; w < total; w += BLOCK_THREADS, sp.next()) {
+        const int le = list ? list[sp.li] : sp.li;
+        const int c = sp.c;
+        const uint32_t rp = s_rp[le];
+        const int ax = rp & 0xFF, ay = (rp >> 8) & 0xFF, dir = (rp >> 16) & 3;
+        const uint8_t carry = (uint8_t)(rp >> 24);
+        const int vx = (c * 37) >> 8, vy = c - vx * 7;          // c / 7 for c < 49
+        const int dx = (dir == 0) - (dir == 2), dy = (dir == 1) - (dir == 3);
+        uint8_t code;
+        if (c == 3 * 7 + 6) {
+            code = carry ? carry : CODE_EMPTY;
+        } else {
+            const int wx = ax + (6 - vy) * dx - (vx - 3) * dy;   // right_vec = (-dy, dx)
+            const int wy = ay + (6 - vy) * dy + (vx - 3) * dx;
+            const bool in = (unsigned)wx < (unsigned)S && (unsigned)wy < (unsigned)S;
+            code = in ? s_grid[le * GSL + wy * S + wx] : CODE_WALL;
+        }
+        const uint32_t v = encode3(code);
+        uint8_t *fr = s_fr + le * FSTRIDE + FOFF;
+        fr[c] = (uint8_t)v;
+        fr[49 + c] = (uint8_t)(v >> 8);
+        fr[98 + c] = (uint8_t)(v >> 16);
+    }
+}
+
+// One vectorised env step of 64 envs per 256-thread workgroup.  No RNG work
+// happens here: auto-resets pop pre-generated episodes from the env's ring
+// (mgx_refill_kernel); an empty ring defers the env to mgx_fixup_kernel, which
+// runs right after on the same stream.  Keeping the generator out of this
+// kernel keeps it register-light (high occupancy hides its memory latency).
 template <typename ActT>
 __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut o, const ActT *__restrict__ actions) {
     extern __shared__ __align__(16) uint8_t smem[];
-    uint8_t *s_stk = smem;                       // image stacks [64][img_bytes]; later reset scratch
-    uint8_t *s_grid = smem + p.stk_lds;          // grids [64][GSL]
+    // fast path (n_stack == 4): smem = frame rows [64][148] (new frame at bytes 1..147);
+    // staged path: smem = image stacks [64][IMG] (new frame in slot 0 of a row).
+    const bool fast = p.fast_roll;
+    uint8_t *s_stk = smem;
+    uint8_t *s_grid = smem + p.stk_step;         // grids [64][GSL]
+    const int IMG = p.img_bytes;
+    const int FSTRIDE = fast ? FROW : IMG, FOFF = fast ? 1 : 0;
+    __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params ax | ay<<8 | dir<<16 | carry<<24
     __shared__ uint8_t s_done[BLOCK_ENVS];
     __shared__ uint8_t s_dirty[BLOCK_ENVS];
-    __shared__ uint8_t s_term_out[BLOCK_ENVS];   // write terminal image stack
-    __shared__ unsigned long long s_ndone, s_ll, s_maxcur;
-    __shared__ uint32_t s_err;
+    __shared__ uint8_t s_dlist[BLOCK_ENVS];
+    __shared__ int s_nd, s_npop;
+    __shared__ unsigned long long s_ll;
 
     const int tid = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * BLOCK_ENVS;
     const int ne = (int)min<int64_t>(BLOCK_ENVS, p.n - e0);
-    const int IMG = p.img_bytes;
-    if (tid == 0) { s_ndone = 0; s_ll = 0; s_maxcur = 0; s_err = 0; }
+    const int S = p.S;
+    if (tid == 0) { s_nd = 0; s_npop = 0; s_ll = 0; }
 #ifdef MGX_STAMPS
     const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-    unsigned long long ts1 = 0, ts2 = 0, ts3 = 0;
+    unsigned long long ts1 = 0, ts2 = 0;
 #endif
 
-    // ---- phase 1: stage grids + image stacks (slot 0 of each env is dead: skip it)
-    grid_copy_in(s_grid, p.grid + e0 * p.GS, ne, p.GS, p.GSL);
+    // ---- phase 1: issue every independent load up front --------------------------
+    // (a) this lane's env state + action (wave 0)
+    EnvState st;
+    int a = 0;
+    if (tid < ne) { st = p.state[e0 + tid]; a = (int)actions[e0 + tid]; }
+    // (b) fast roll: the old image-stack dwords this lane's output quads need, into registers
+    constexpr int DW = FRAME_DW4;                                                     // 147
+    constexpr int MAXQ = (BLOCK_ENVS * DW / 4 + BLOCK_THREADS - 1) / BLOCK_THREADS;  // 10
+    const uint32_t *g32in = reinterpret_cast<const uint32_t *>(o.img + e0 * (int64_t)IMG);
+    const int limit = ne * DW;
+    const int nq = fast ? (limit >> 2) : 0;
+    uint4 qa[MAXQ];
+    uint32_t qb[MAXQ];
+    if (fast) {
+#pragma unroll
+        for (int r = 0; r < MAXQ; r++) {
+            const int q = r * BLOCK_THREADS + tid, k = 4 * q;
+            qa[r] = make_uint4(0, 0, 0, 0);
+            qb[r] = 0;
+            if (q < nq) {
+                if (k + 39 < limit) {
+                    qa[r] = *reinterpret_cast<const uint4 *>(g32in + k + 36);          // 16-B aligned
+                } else {                                                               // last row: stay inside
+                    if (k + 36 < limit) qa[r].x = g32in[k + 36];
+                    if (k + 37 < limit) qa[r].y = g32in[k + 37];
+                    if (k + 38 < limit) qa[r].z = g32in[k + 38];
+                }
+                if (k + 40 < limit) qb[r] = g32in[k + 40];
+            }
+        }
+    }
+    // (c) grids -> LDS (and, staged path, the whole old stacks -> LDS)
     {
+        const int q = p.GS >> 4;
+        const int n16 = ne * q;
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.grid + e0 * p.GS);
+        for (int base = 0; base < n16; base += 4 * BLOCK_THREADS) {
+            uint4 v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = src[min(base + j * BLOCK_THREADS + tid, n16 - 1)];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int i = base + j * BLOCK_THREADS + tid;
+                if (i < n16) {
+                    const int e = i / q, c = i - e * q;
+                    uint32_t *d = reinterpret_cast<uint32_t *>(s_grid + e * p.GSL + c * 16);
+                    d[0] = v[j].x; d[1] = v[j].y; d[2] = v[j].z; d[3] = v[j].w;
+                }
+            }
+        }
+    }
+    if (!fast) {
         const uint8_t *gimg = o.img + e0 * (int64_t)IMG;
         const int nbytes = ne * IMG;
         const int n16 = nbytes >> 4;
         const uint4 *src = reinterpret_cast<const uint4 *>(gimg);
         uint4 *dst = reinterpret_cast<uint4 *>(s_stk);
-        for (int i = tid; i < n16; i += BLOCK_THREADS) {
-            int b0 = i << 4;
-            int off = b0 % IMG;
-            // chunk entirely inside slot 0 of one env -> not needed
-            if (off + 16 <= FRAME) continue;
-            dst[i] = src[i];
-        }
+        for (int i = tid; i < n16; i += BLOCK_THREADS) dst[i] = src[i];
         for (int i = (n16 << 4) + tid; i < nbytes; i += BLOCK_THREADS) s_stk[i] = gimg[i];
     }
     __syncthreads();
+#ifdef MGX_STAMPS
+    ts1 = __builtin_amdgcn_s_memtime();
+#endif
 
-    // ---- phase 2: one lane per env: MiniGridEnv.step + PlaygroundEnv.step
-    EnvState st;
-    bool done = false;
+    // ---- phase 2a: one lane per env: MiniGridEnv.step + PlaygroundEnv.step
     uint32_t my_err = 0;
+    bool done = false, term = false, trunc = false, dirty = false;
+    int mdone = 0, rs = -1, dir = 0;
     if (tid < ne) {
         const int64_t e = e0 + tid;
-        st = p.state[e];
-        int a = (int)actions[e];
         if ((unsigned)a > 6u) { my_err |= MGX_DEVERR_BAD_ACTION; a = -1; }
         uint8_t *g = s_grid + tid * p.GSL;
-        const int S = p.S, ms = S * S;
+        const int ms = S * S;
         const int sc = st.step_count + 1;
-        int ax = st.ax, ay = st.ay, dir = st.dir;
+        int ax = st.ax, ay = st.ay;
+        dir = st.dir;
         uint8_t carry = st.carry;
         const int fx = ax + ((dir == 0) - (dir == 2)), fy = ay + ((dir == 1) - (dir == 3));
         uint8_t *fp = g + fy * S + fx;
         const uint8_t fc = *fp;
         const int ft = fc & 15;
-        bool term = false, dirty = false;
         double rew = 0.0;
         switch (a) {                                   // MiniGridEnv.step (3P)
             case A_LEFT: dir = (dir + 3) & 3; break;
@@ -319,7 +453,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                 break;
             case A_TOGGLE:
                 if (ft == T_DOOR) {
-                    if (fc >> 7) {                     // locked
+                    if (fc >> 7) {                     // locked: needs a Key of the door's colour
                         if ((carry & 15) == T_KEY && ((carry >> 4) & 7) == ((fc >> 4) & 7)) {
                             *fp = mk_code(T_OPEN, (fc >> 4) & 7, 0); dirty = true;
                         }
@@ -332,16 +466,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                 break;
             default: break;                            // done (and invalid) -> no-op
         }
-        const bool trunc = sc >= ms;
-        // gen_obs() happens here, before PlaygroundEnv's key consumption (Q3)
-        uint8_t *fr = s_stk + tid * IMG;               // dead slot 0 -> rotated to newest below
-        render_view(g, S, ax, ay, dir, carry, [&](int k, uint32_t v) {
-            fr[k] = (uint8_t)v;
-            fr[49 + k] = (uint8_t)(v >> 8);
-            fr[98 + k] = (uint8_t)(v >> 16);
-        });
+        trunc = sc >= ms;
+        // gen_obs() is taken here, before PlaygroundEnv's key consumption (Q3)
+        s_rp[tid] = (uint32_t)ax | ((uint32_t)ay << 8) | ((uint32_t)dir << 16) | ((uint32_t)carry << 24);
         // ---- PlaygroundEnv.step (custom_env.py:269-330)
-        int mdone = st.mission_done, rs = st.reward_step;
+        mdone = st.mission_done;
+        rs = st.reward_step;
         const bool is_gtg = st.mission_id == CMD_GOTOGOAL;
         if (term) {
             if (!is_gtg) { mdone = 0; rs = -1; rew = 0.0; }
@@ -378,136 +508,288 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         if (o.done) o.done[e] = done;
         if (o.ep_ret) o.ep_ret[e] = (float)rew;       // only the final step can pay a reward
         if (o.ep_len) o.ep_len[e] = sc;
-        if (o.livelock) o.livelock[e] = 0;
-        const bool want_term = done && (p.terminal_mode == MGX_TERMINAL_ALL ||
-                                        (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term));
-        const int frames = min((int)st.frames + 1, p.n_stack);
-        const uint8_t *tok = p.mtok + st.mission_id * 32;
         if (!done) {
+            const int frames = min((int)st.frames + 1, p.n_stack);
             dir_stack_roll(o.dir, o.dir, e, p.n_stack, dir);
             if (st.frames < p.n_stack)                 // stack still filling: one slot flips 0 -> mission
-                write_mission_slot(o.mis, p.mission64, e, p.n_stack, p.n_stack - frames, tok);
+                write_mission_slot(o.mis, p.mission64, e, p.n_stack, p.n_stack - frames, p.mtok + st.mission_id * 32);
             st.ax = (uint8_t)ax; st.ay = (uint8_t)ay; st.dir = (uint8_t)dir; st.carry = carry;
             st.step_count = (uint16_t)sc; st.reward_step = (int16_t)rs; st.mission_done = (uint8_t)mdone;
             st.frames = (uint8_t)frames;
             p.state[e] = st;
+            if (o.livelock) o.livelock[e] = 0;
         } else {
-            if (want_term) {
-                dir_stack_roll(o.dir, o.t_dir, e, p.n_stack, dir);
-                write_mission_stack(o.t_mis, p.mission64, e, p.n_stack, frames, tok);
-            }
-            // survives the reset (Q2): mission_done / stored reward
-            st.reward_step = (int16_t)rs; st.mission_done = (uint8_t)mdone;
+            s_dlist[atomicAdd(&s_nd, 1)] = (uint8_t)tid;
         }
         s_done[tid] = done;
-        s_dirty[tid] = dirty;
-        s_term_out[tid] = want_term;
-        if (done) atomicAdd(&s_ndone, 1ull);
     } else if (tid < BLOCK_ENVS) {
-        s_done[tid] = 0; s_dirty[tid] = 0; s_term_out[tid] = 0;
+        s_done[tid] = 0;
     }
     __syncthreads();
-#ifdef MGX_STAMPS
-    ts1 = __builtin_amdgcn_s_memtime();
-#endif
 
-    // ---- phase 3: write the rolled image stacks (newest frame sits in slot 0 of LDS)
-    {
-        uint8_t *gimg = o.img + e0 * (int64_t)IMG;
-        if ((IMG & 3) == 0) {
-            // dword path (n_stack % 4 == 0): out byte o = lds[(o + 147) mod IMG]
-            //   -> out dword j = alignbyte(dw[(j+37) mod DW], dw[(j+36) mod DW], 3)
-            const int DW = IMG >> 2;
-            const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s_stk);
-            uint32_t *g32 = reinterpret_cast<uint32_t *>(gimg);
-            for (int k = tid; k < ne * DW; k += BLOCK_THREADS) {
-                const int e = k / DW, j = k - e * DW;
-                uint32_t out = 0;
-                if (!s_done[e]) {
-                    int j0 = j + FRAME / 4;
-                    if (j0 >= DW) j0 -= DW;
-                    const int j1 = (j0 + 1 == DW) ? 0 : j0 + 1;
-                    out = __builtin_amdgcn_alignbyte(s32[e * DW + j1], s32[e * DW + j0], FRAME & 3);
-                }
-                g32[k] = out;
+    // ---- phase 2b: render every env's frame (all 256 threads)
+    render_block(s_grid, s_stk, s_rp, nullptr, ne, S, p.GSL, FSTRIDE, FOFF);
+    __syncthreads();
+
+    // ---- phase 2c: done envs: terminal_observation, then auto-reset from the ring
+    const int nd = s_nd;
+    if (nd) {
+        if (tid < ne && done) {
+            const int64_t e = e0 + tid;
+            const uint8_t *fr = s_stk + tid * FSTRIDE + FOFF;    // terminal frame
+            const int frames = min((int)st.frames + 1, p.n_stack);
+            if (p.terminal_mode == MGX_TERMINAL_ALL || (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term)) {
+                // re-stacked like VecFrameStack (rare -> per-lane writes): older frames, then the terminal one
+                uint8_t *t = o.t_img + e * (int64_t)IMG;
+                const uint8_t *old = fast ? o.img + e * (int64_t)IMG : s_stk + tid * IMG;
+                for (int off = 0; off < IMG - FRAME; off++) t[off] = old[off + FRAME];
+                for (int k = 0; k < FRAME; k++) t[IMG - FRAME + k] = fr[k];
+                dir_stack_roll(o.dir, o.t_dir, e, p.n_stack, dir);
+                write_mission_stack(o.t_mis, p.mission64, e, p.n_stack, frames, p.mtok + st.mission_id * 32);
             }
-        } else {
-            const int nbytes = ne * IMG;
-            for (int b = tid; b < nbytes; b += BLOCK_THREADS) {
-                const int e = b / IMG, off = b - e * IMG;
-                int src = off + FRAME;
-                if (src >= IMG) src -= IMG;
-                gimg[b] = s_done[e] ? 0 : s_stk[e * IMG + src];
+            // SubprocVecEnv auto-reset: env.reset() (unseeded): pop the next pre-generated episode
+            uint8_t *g = s_grid + tid * p.GSL;
+            const uint16_t ctl = p.ring_ctl[e];
+            int head = ctl & 0xFF, cnt = ctl >> 8;
+            if (cnt > 0) {
+                const int64_t slot = e * p.D + head;
+                const uint4 h = p.ring_hdr[slot];
+                const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
+                for (int c = 0; c < (p.GS >> 4); c++) {
+                    const uint4 v = gsrc[c];
+                    uint32_t *d = reinterpret_cast<uint32_t *>(g + c * 16);
+                    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+                }
+                p.cur_rng[2 * e] = p.ring_rng[2 * slot];
+                p.cur_rng[2 * e + 1] = p.ring_rng[2 * slot + 1];
+                head = head + 1 == p.D ? 0 : head + 1;
+                p.ring_ctl[e] = (uint16_t)(head | ((cnt - 1) << 8));
+                const int nax = h.x & 0xFF, nay = (h.x >> 8) & 0xFF, ndir = (h.x >> 16) & 0xFF;
+                const uint8_t mid = (uint8_t)(h.y >> 16);
+                EnvState ns;
+                ns.ax = (uint8_t)nax; ns.ay = (uint8_t)nay; ns.dir = (uint8_t)ndir; ns.carry = 0;
+                ns.step_count = 0; ns.reward_step = (int16_t)rs;          // survives the reset (Q2)
+                ns.tx = (uint8_t)(h.x >> 24); ns.ty = (uint8_t)h.y; ns.target_action = (uint8_t)(h.y >> 8);
+                ns.mission_id = mid;
+                ns.mission_done = (uint8_t)mdone; ns.frames = 1; ns.flags = 0; ns.pad = 0;
+                p.state[e] = ns;
+                s_rp[tid] = (uint32_t)nax | ((uint32_t)nay << 8) | ((uint32_t)ndir << 16);
+                dir_stack_fresh(o.dir, e, p.n_stack, ndir);
+                write_mission_stack(o.mis, p.mission64, e, p.n_stack, 1, p.mtok + mid * 32);
+                if (o.livelock) o.livelock[e] = (int)h.z;
+                dirty = true;
+                atomicAdd(&s_ll, (unsigned long long)h.z);
+                s_dlist[atomicAdd(&s_npop, 1)] = (uint8_t)tid;   // re-used as the render list (nd >= npop)
+            } else {
+                // empty ring: mgx_fixup_kernel generates this env's episode inline.  Keep the
+                // episode-spanning flags (Q2) in the state it will complete.
+                st.reward_step = (int16_t)rs; st.mission_done = (uint8_t)mdone;
+                p.state[e] = st;
+                p.fix_list[atomicAdd(p.fix_count, 1u)] = (uint32_t)e;
             }
         }
-        // terminal stacks (rare: done envs that asked for one)
-        if (p.terminal_mode != MGX_TERMINAL_NONE && s_ndone) {
-            for (int le = 0; le < ne; le++) {
-                if (!s_term_out[le]) continue;
-                uint8_t *dst = o.t_img + (e0 + le) * (int64_t)IMG;
-                for (int off = tid; off < IMG; off += BLOCK_THREADS) {
-                    int src = off + FRAME;
-                    if (src >= IMG) src -= IMG;
-                    dst[off] = s_stk[le * IMG + src];
-                }
-            }
-        }
+        __syncthreads();
+        // first frames of the new episodes -> frame rows (phase 3 zero-fills the older slots)
+        render_block(s_grid, s_stk, s_rp, s_dlist, s_npop, S, p.GSL, FSTRIDE, FOFF);
     }
+    if (tid < BLOCK_ENVS) s_dirty[tid] = dirty;
+    if (my_err) atomicOr(p.err, my_err);
     __syncthreads();
 #ifdef MGX_STAMPS
     ts2 = __builtin_amdgcn_s_memtime();
 #endif
 
-    // ---- phase 4: fused auto-reset of done envs (SubprocVecEnv: env.reset() unseeded)
-    if (s_ndone) {
-        if (tid < ne && done) {
-            const int64_t e = e0 + tid;
-            Gen G;
-            load_gen(G, p, e, s_grid + tid * p.GSL, s_stk, tid);
-            load_rng(G, p, e);
-            ResetOut R;
-            reset_env(G, R);
-            EnvState ns;
-            ns.ax = (uint8_t)G.ax; ns.ay = (uint8_t)G.ay; ns.dir = (uint8_t)G.adir; ns.carry = 0;
-            ns.step_count = 0; ns.reward_step = st.reward_step;
-            ns.tx = R.tx; ns.ty = R.ty; ns.target_action = R.ta; ns.mission_id = R.mission_id;
-            ns.mission_done = st.mission_done; ns.frames = 1; ns.flags = 0; ns.pad = 0;
-            p.state[e] = ns;
-            store_rng(G, p, e);
-            write_fresh_frame(p, o.img, e, G.g, G.ax, G.ay, G.adir);
-            dir_stack_fresh(o.dir, e, p.n_stack, G.adir);
-            write_mission_stack(o.mis, p.mission64, e, p.n_stack, 1, p.mtok + R.mission_id * 32);
-            if (o.livelock) o.livelock[e] = R.livelocks;
-            s_dirty[tid] = 1;
-            atomicAdd(&s_ll, (unsigned long long)R.livelocks);
-            atomicMax(&s_maxcur, (unsigned long long)G.cur);
-            my_err |= G.err;
+    // ---- phase 3: roll the image stacks.  out byte o of an env row = its old byte o+147
+    // (o < IMG-147) or the newest frame (o >= IMG-147); done envs: zeros + newest frame.
+    if (fast) {
+        // Block-relative output dword k needs old dwords k+36, k+37 (alignbyte by 3) while its
+        // env column j = k mod 147 <= 109; dword 110 mixes old byte 587 with new bytes 0..2;
+        // dwords >= 111 are new-frame dwords (the LDS frame row holds new byte b at byte 1+b).
+        // The old dwords were loaded into registers in phase 1, before any store: in place, no hazard.
+        const uint32_t *f32 = reinterpret_cast<const uint32_t *>(s_stk);
+        uint4 *g128 = reinterpret_cast<uint4 *>(o.img + e0 * (int64_t)IMG);
+#pragma unroll
+        for (int r = 0; r < MAXQ; r++) {
+            const int q = r * BLOCK_THREADS + tid, k = 4 * q;
+            if (q < nq) {
+                const uint32_t src[5] = {qa[r].x, qa[r].y, qa[r].z, qa[r].w, qb[r]};
+                int e = k / DW, j = k - e * DW;
+                uint32_t w[4];
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const bool dn = s_done[e];
+                    uint32_t out;
+                    if (j <= 109) out = dn ? 0u : __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
+                    else if (j == 110) out = (f32[e * (FROW / 4)] & 0xFFFFFF00u) | (dn ? 0u : (src[t] >> 24));
+                    else out = f32[e * (FROW / 4) + (j - 110)];
+                    w[t] = out;
+                    if (++j == DW) { j = 0; e++; }
+                }
+                g128[q] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
         }
-        __syncthreads();
+        // tail dword (partial last block whose row count is not a multiple of 4): its old
+        // dwords come from rows no other thread of this block writes before the barrier below
+        if (limit != nq * 4) {
+            const int kt = nq * 4 + tid;
+            uint32_t tv = 0;
+            if (kt < limit) {
+                const int e = kt / DW, j = kt - e * DW;
+                const bool dn = s_done[e];
+                if (j <= 109) tv = dn ? 0u : __builtin_amdgcn_alignbyte(g32in[kt + 37], g32in[kt + 36], 3);
+                else if (j == 110) tv = (f32[e * (FROW / 4)] & 0xFFFFFF00u) | (dn ? 0u : (g32in[kt + 36] >> 24));
+                else tv = f32[e * (FROW / 4) + (j - 110)];
+            }
+            __syncthreads();
+            if (kt < limit) reinterpret_cast<uint32_t *>(o.img + e0 * (int64_t)IMG)[kt] = tv;
+        }
+    } else {
+        uint8_t *gimg = o.img + e0 * (int64_t)IMG;
+        const int NEWEST = IMG - FRAME;
+        const int nbytes = ne * IMG;
+        for (int b = tid; b < nbytes; b += BLOCK_THREADS) {
+            const int e = b / IMG, off = b - e * IMG;
+            int src = off + FRAME;
+            if (src >= IMG) src -= IMG;
+            gimg[b] = (s_done[e] && off < NEWEST) ? 0 : s_stk[e * IMG + src];
+        }
     }
-    if (my_err) atomicOr(&s_err, my_err);
-#ifdef MGX_STAMPS
-    ts3 = __builtin_amdgcn_s_memtime();
-#endif
 
-    // ---- phase 5: write back grids that changed
+    // ---- phase 5: write back grids that changed (moves, pickups, resets)
     grid_copy_out(p.grid + e0 * p.GS, s_grid, ne, p.GS, p.GSL, s_dirty);
-    __syncthreads();
     if (tid == 0) {
-        atomicAdd(&p.counters[0], (unsigned long long)ne);
-        if (s_ndone) {
-            atomicAdd(&p.counters[1], s_ndone);
-            atomicAdd(&p.counters[2], s_ll);
-            atomicMax(&p.counters[3], s_maxcur);
-        }
-        if (s_err) atomicOr(p.err, s_err);
+        ulonglong4 b = p.blk[blockIdx.x];           // workgroup-private stats slot (no contention)
+        b.x += (unsigned long long)ne; b.y += (unsigned long long)nd; b.z += s_ll;
+        p.blk[blockIdx.x] = b;
 #ifdef MGX_STAMPS
         const unsigned long long ts4 = __builtin_amdgcn_s_memtime();
-        atomicAdd(&p.counters[4], ts1 - ts0);   // phase 1+2: stage + step logic
-        atomicAdd(&p.counters[5], ts2 - ts1);   // phase 3: stack roll write-back
-        atomicAdd(&p.counters[6], ts3 - ts2);   // phase 4: fused resets
-        atomicAdd(&p.counters[7], ts4 - ts3);   // phase 5: grid write-back
+        atomicAdd(&p.counters[4], ts1 - ts0);   // phase 1: loads
+        atomicAdd(&p.counters[5], ts2 - ts1);   // phase 2: step + render + resets
+        atomicAdd(&p.counters[6], ts4 - ts2);   // phase 3+5: stack + grid write-back
 #endif
+    }
+}
+
+// ============================================================== fixup kernel
+// Generates, inline, the next episode of every env the step kernel found with an
+// empty ring (normally none; every done env when the ring is disabled), and writes
+// that env's reset outputs.  Grid-stride over the list; the last workgroup to
+// finish clears the list for the next step.
+template <int NW>
+__global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    const int tid = threadIdx.x;
+    uint8_t *s_grid = smem;                                   // [64][GSL]
+    uint8_t *s_scr = smem + ((64 * p.GSL + 15) & ~15);        // [64] windows + objs
+    const uint32_t cnt = *reinterpret_cast<volatile uint32_t *>(p.fix_count);
+    unsigned long long ll = 0, maxcur = 0;
+    uint32_t err = 0;
+    for (uint32_t idx = blockIdx.x * 64 + tid; idx < cnt; idx += gridDim.x * 64) {
+        const int64_t e = p.fix_list[idx];
+        Gen<NW> G;
+        load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
+        load_rng(G, p, e);
+        ResetOut R;
+        reset_env(G, R);
+        store_rng(G, p, e);
+        rng_snapshot(G, p.cur_rng + 2 * e);
+        {
+            uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e * p.GS);
+            for (int c = 0; c < (p.GS >> 4); c++) {
+                const uint32_t *q = reinterpret_cast<const uint32_t *>(G.g + c * 16);
+                dst[c] = make_uint4(q[0], q[1], q[2], q[3]);
+            }
+        }
+        EnvState ns = p.state[e];                  // carries mission_done / stored reward (Q2)
+        ns.ax = (uint8_t)G.ax; ns.ay = (uint8_t)G.ay; ns.dir = (uint8_t)G.adir; ns.carry = 0;
+        ns.step_count = 0;
+        ns.tx = R.tx; ns.ty = R.ty; ns.target_action = R.ta; ns.mission_id = R.mission_id;
+        ns.frames = 1; ns.flags = 0; ns.pad = 0;
+        p.state[e] = ns;
+        write_fresh_frame(p, o.img, e, G.g, G.ax, G.ay, G.adir);   // older slots were zeroed by the step
+        dir_stack_fresh(o.dir, e, p.n_stack, G.adir);
+        write_mission_stack(o.mis, p.mission64, e, p.n_stack, 1, p.mtok + R.mission_id * 32);
+        if (o.livelock) o.livelock[e] = R.livelocks;
+        ll += (unsigned long long)R.livelocks;
+        maxcur = G.cur > maxcur ? G.cur : maxcur;
+        err |= G.err;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        ll += __shfl_down(ll, off);
+        const unsigned long long m = __shfl_down(maxcur, off);
+        maxcur = m > maxcur ? m : maxcur;
+        err |= __shfl_down(err, off);
+    }
+    if (tid == 0 && cnt) {                                     // nothing listed: no bookkeeping at all
+        ulonglong4 b = p.blk[p.nblk + blockIdx.x];
+        b.z += ll; b.w = b.w > maxcur ? b.w : maxcur;
+        p.blk[p.nblk + blockIdx.x] = b;
+        if (err) atomicOr(p.err, err);
+        __threadfence();
+        if (atomicAdd(p.fix_done, 1u) == gridDim.x - 1) {   // every workgroup has read `cnt`
+            *p.fix_count = 0;
+            *p.fix_done = 0;
+        }
+    }
+}
+
+// ============================================================= refill kernel
+// Pre-generates each env's next episodes into its ring until it holds D.
+// Generation is a long serial RNG chain per env (~10^4 dependent ops); doing
+// it here, batched every `refill_every` steps for all envs at once, takes it
+// off the step kernel's critical path.  Episodes are generated in exactly the
+// order the env will consume them, so RNG streams advance as in the reference.
+// One wave per workgroup; all LDS is lane-private (grid row + MT window + objs).
+template <int NW>
+__global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    const int tid = threadIdx.x;
+    const int64_t e = (int64_t)blockIdx.x * 64 + tid;
+    uint8_t *s_grid = smem;                                   // [64][GSL]
+    uint8_t *s_scr = smem + ((64 * p.GSL + 15) & ~15);        // [64] windows + objs
+    unsigned long long maxcur = 0;
+    uint32_t err = 0;
+    if (e < p.n) {
+        const uint16_t ctl = p.ring_ctl[e];
+        const int head = ctl & 0xFF;
+        int cnt = ctl >> 8;
+        if (cnt < p.D) {
+            Gen<NW> G;
+            load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
+            load_rng(G, p, e);
+            while (cnt < p.D) {
+                ResetOut R;
+                reset_env(G, R);
+                int k = head + cnt;
+                if (k >= p.D) k -= p.D;
+                const int64_t slot = e * p.D + k;
+                uint4 *dst = reinterpret_cast<uint4 *>(p.ring_grid + slot * p.GS);
+                for (int c = 0; c < (p.GS >> 4); c++) {
+                    const uint32_t *q = reinterpret_cast<const uint32_t *>(G.g + c * 16);
+                    dst[c] = make_uint4(q[0], q[1], q[2], q[3]);
+                }
+                p.ring_hdr[slot] = pack_hdr(G, R);
+                rng_snapshot(G, p.ring_rng + 2 * slot);
+                cnt++;
+            }
+            store_rng(G, p, e);
+            p.ring_ctl[e] = (uint16_t)(head | (cnt << 8));
+            maxcur = G.cur;
+            err = G.err;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        unsigned long long o = __shfl_down(maxcur, off);
+        maxcur = o > maxcur ? o : maxcur;
+        err |= __shfl_down(err, off);
+    }
+    if (tid == 0) {
+        if (maxcur) {
+            ulonglong4 b = p.blk[2 * p.nblk + blockIdx.x];
+            b.w = b.w > maxcur ? b.w : maxcur;
+            p.blk[2 * p.nblk + blockIdx.x] = b;
+        }
+        if (err) atomicOr(p.err, err);
     }
 }
 
@@ -663,8 +945,10 @@ struct mgx_handle {
     mgx_config cfg;
     int device;
     KParams kp;
-    size_t lds_step, lds_reset;
-    void *allocs[8];
+    size_t lds_step, lds_reset, lds_refill;
+    int nw;                 // 64-bit words of the generator's S*S cell masks (1, 2 or 4)
+    int refill_every, since_refill;
+    void *allocs[16];
 };
 
 extern "C" {
@@ -725,6 +1009,12 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->cfg = *cfg;
     h->device = device;
     if (h->cfg.livelock_words <= 0) h->cfg.livelock_words = MGX_LIVELOCK_WORDS;
+    if (h->cfg.ring_depth == 0) h->cfg.ring_depth = 64;
+    if (h->cfg.ring_depth < 0) h->cfg.ring_depth = 0;          // ring disabled: every reset generated inline
+    if (h->cfg.ring_depth > 255) h->cfg.ring_depth = 255;
+    if (h->cfg.refill_every <= 0 || h->cfg.refill_every > h->cfg.ring_depth) h->cfg.refill_every = h->cfg.ring_depth;
+    h->refill_every = h->cfg.refill_every;
+    h->since_refill = 0;
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 24;
     h->cfg.mt_table_words = (h->cfg.mt_table_words + 3) & ~(int64_t)3;
     const int64_t N = cfg->n_envs;
@@ -744,6 +1034,20 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     for (int i = 0; i < 6; i++) {
         hipError_t e = hipMalloc(&h->allocs[i], sizes[i]);
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e)));
+    }
+    const int D = h->cfg.ring_depth;
+    {
+        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 16, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 2};
+        for (int i = 0; i < 5; i++) {
+            hipError_t e = hipMalloc(&h->allocs[7 + i], rs[i] ? rs[i] : 16);
+            if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, std::string("hipMalloc ring: ") + hipGetErrorString(e)));
+        }
+        hipError_t e = hipMemset(h->allocs[11], 0, (size_t)N * 2);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset ring ctl"));
+        e = hipMalloc(&h->allocs[12], (size_t)N * 4 + 64);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc fix list"));
+        e = hipMemset(h->allocs[12], 0, (size_t)N * 4 + 64);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset fix list"));
     }
     {
         hipError_t e = hipMalloc(&h->allocs[6], 8 * sizeof(unsigned long long) + 64);
@@ -787,19 +1091,48 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.n_stack = cfg->n_stack;
     p.img_bytes = IMG;
     const int scratch = BLOCK_ENVS * SCRATCH_PER_ENV;
-    p.stk_lds = (std::max(BLOCK_ENVS * IMG, scratch) + 15) & ~15;
+    p.stk_lds = (std::max(BLOCK_ENVS * IMG, scratch) + 15) & ~15;   // reset kernel: stack area doubles as scratch
+    p.grid_lds = (BLOCK_ENVS * (GS + 4) + 15) & ~15;
+    p.fast_roll = cfg->n_stack == 4;
+    p.stk_step = p.fast_roll ? (BLOCK_ENVS * FROW + 15) & ~15 : (BLOCK_ENVS * IMG + 15) & ~15;
     p.problem = cfg->problem;
     p.cfg_mission = cfg->mission;
     p.num_objects = cfg->num_objects;
     p.all_doors_open = cfg->all_doors_open;
     p.llw = (uint32_t)h->cfg.livelock_words;
     p.terminal_mode = cfg->terminal_mode;
+    p.ring_grid = (uint8_t *)h->allocs[7];
+    p.ring_hdr = (uint4 *)h->allocs[8];
+    p.ring_rng = (uint4 *)h->allocs[9];
+    p.cur_rng = (uint4 *)h->allocs[10];
+    p.ring_ctl = (uint16_t *)h->allocs[11];
+    p.fix_list = (uint32_t *)h->allocs[12];
+    p.fix_count = p.fix_list + N + 4;       // 16-B aligned tail of the same allocation
+    p.fix_done = p.fix_list + N + 8;
+    p.nblk = (int)((N + 63) / 64);
+    {
+        hipError_t e = hipMalloc(&h->allocs[13], (size_t)3 * p.nblk * sizeof(ulonglong4));
+        if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc stats"));
+        e = hipMemset(h->allocs[13], 0, (size_t)3 * p.nblk * sizeof(ulonglong4));
+        if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset stats"));
+        p.blk = (ulonglong4 *)h->allocs[13];
+    }
+    p.D = D;
     p.mission64 = cfg->mission_int64;
-    h->lds_step = (size_t)p.stk_lds + (size_t)BLOCK_ENVS * (GS + 4);
-    h->lds_reset = h->lds_step;
+    h->lds_step = (size_t)p.stk_step + (size_t)p.grid_lds;
+    h->lds_reset = (size_t)p.stk_lds + (size_t)p.grid_lds;
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
-    HIP_TRY(hipFuncSetAttribute((const void *)mgx_reset_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_reset));
+    h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
+#define MGX_SET_LDS(K, bytes)                                                                            \
+    HIP_TRY(hipFuncSetAttribute((const void *)K<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes))); \
+    HIP_TRY(hipFuncSetAttribute((const void *)K<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes))); \
+    HIP_TRY(hipFuncSetAttribute((const void *)K<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes)))
+    MGX_SET_LDS(mgx_reset_kernel, h->lds_reset);
+    h->lds_refill = (size_t)((64 * (GS + 4) + 15) & ~15) + (size_t)64 * SCRATCH_PER_ENV;
+    MGX_SET_LDS(mgx_refill_kernel, h->lds_refill);
+    MGX_SET_LDS(mgx_fixup_kernel, h->lds_refill);
+#undef MGX_SET_LDS
     (void)hipSetDevice(prev);
     *out = h;
     return MGX_OK;
@@ -813,6 +1146,19 @@ mgx_status mgx_destroy(mgx_handle *h) {
     for (void *&p : h->allocs) if (p) { (void)hipFree(p); p = nullptr; }
     (void)hipSetDevice(prev);
     delete h;
+    return MGX_OK;
+}
+
+static mgx_status launch_refill(mgx_handle *h, void *stream) {
+    if (h->kp.D == 0) return MGX_OK;
+    const int64_t nblk = (h->kp.n + 63) / 64;
+    switch (h->nw) {
+        case 1: hipLaunchKernelGGL(mgx_refill_kernel<1>, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp); break;
+        case 2: hipLaunchKernelGGL(mgx_refill_kernel<2>, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp); break;
+        default: hipLaunchKernelGGL(mgx_refill_kernel<4>, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp); break;
+    }
+    HIP_TRY(hipGetLastError());
+    h->since_refill = 0;
     return MGX_OK;
 }
 
@@ -845,10 +1191,13 @@ mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, v
     KOut o = make_out(obs, nullptr);
     o.livelock = livelock_dev;
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
-    hipLaunchKernelGGL(mgx_reset_kernel, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset,
-                       (hipStream_t)stream, h->kp, o);
+    switch (h->nw) {
+        case 1: hipLaunchKernelGGL(mgx_reset_kernel<1>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
+        case 2: hipLaunchKernelGGL(mgx_reset_kernel<2>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
+        default: hipLaunchKernelGGL(mgx_reset_kernel<4>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
+    }
     HIP_TRY(hipGetLastError());
-    return MGX_OK;
+    return launch_refill(h, stream);
 }
 
 mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, const mgx_step_out *out, void *stream) {
@@ -870,6 +1219,16 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
     else
         return fail(MGX_ERR_INVALID, "action_bytes must be 4 or 8");
     HIP_TRY(hipGetLastError());
+    {   // envs whose ring ran dry (every done env when the ring is disabled)
+        const unsigned fblk = h->kp.D > 0 ? (unsigned)std::min(16, h->kp.nblk) : (unsigned)h->kp.nblk;
+        switch (h->nw) {
+            case 1: hipLaunchKernelGGL(mgx_fixup_kernel<1>, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o); break;
+            case 2: hipLaunchKernelGGL(mgx_fixup_kernel<2>, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o); break;
+            default: hipLaunchKernelGGL(mgx_fixup_kernel<4>, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o); break;
+        }
+        HIP_TRY(hipGetLastError());
+    }
+    if (h->kp.D > 0 && ++h->since_refill >= h->refill_every) return launch_refill(h, stream);
     return MGX_OK;
 }
 
@@ -901,6 +1260,10 @@ mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[4]) {
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     unsigned long long c[8];
     HIP_TRY(hipMemcpy(c, h->kp.counters, sizeof c, hipMemcpyDeviceToHost));
+    std::vector<ulonglong4> b((size_t)3 * h->kp.nblk);
+    HIP_TRY(hipMemcpy(b.data(), h->kp.blk, b.size() * sizeof(ulonglong4), hipMemcpyDeviceToHost));
+    c[0] = c[1] = c[2] = c[3] = 0;
+    for (const ulonglong4 &v : b) { c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] = v.w > c[3] ? v.w : c[3]; }
     for (int i = 0; i < 8; i++) out[i] = c[i];
     return MGX_OK;
 }
@@ -927,12 +1290,12 @@ mgx_status mgx_dump_state(mgx_handle *h, void *stream, uint8_t *grid, uint8_t *a
             for (int x = 0; x < S; x++)
                 for (int y = 0; y < S; y++) enc(g[(size_t)i * GS + y * S + x], grid + (((size_t)i * S + x) * S + y) * 4);
     }
-    std::vector<uint4> pc, ax;
+    std::vector<uint4> pc, cr;
     if (pcg || mt_words) {
         pc.resize((size_t)N * 2);
-        ax.resize((size_t)N);
+        cr.resize((size_t)N * 2);
         HIP_TRY(hipMemcpy(pc.data(), h->kp.pcg, pc.size() * 16, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(ax.data(), h->kp.aux, ax.size() * 16, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(cr.data(), h->kp.cur_rng, cr.size() * 16, hipMemcpyDeviceToHost));
     }
     const int ms = S * S;
     for (int64_t i = 0; i < N; i++) {
@@ -945,9 +1308,9 @@ mgx_status mgx_dump_state(mgx_handle *h, void *stream, uint8_t *grid, uint8_t *a
         if (step_count) step_count[i] = s.step_count;
         if (mission_done) mission_done[i] = s.mission_done;
         if (stored_reward) stored_reward[i] = s.reward_step < 0 ? NAN : 1.0 - 0.9 * ((double)s.reward_step / (double)ms);
-        if (mt_words) mt_words[i] = (int64_t)((uint64_t)ax[(size_t)i].z | ((uint64_t)ax[(size_t)i].w << 32));
+        if (mt_words) mt_words[i] = (int64_t)((uint64_t)cr[(size_t)i * 2 + 1].z | ((uint64_t)cr[(size_t)i * 2 + 1].w << 32));
         if (pcg) {
-            const uint4 a = pc[(size_t)i * 2], b = pc[(size_t)i * 2 + 1], c = ax[(size_t)i];
+            const uint4 a = cr[(size_t)i * 2], b = pc[(size_t)i * 2 + 1], c = cr[(size_t)i * 2 + 1];
             uint64_t *o6 = pcg + i * 6;
             o6[0] = ((uint64_t)a.x << 32) | a.y; o6[1] = ((uint64_t)a.z << 32) | a.w;
             o6[2] = ((uint64_t)b.x << 32) | b.y; o6[3] = ((uint64_t)b.z << 32) | b.w;

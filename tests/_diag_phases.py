@@ -1,5 +1,5 @@
 import sys, time, json
-sys.path[:0] = ['minigrid-rl_amd']
+import os; sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'minigrid-rl_amd')]
 import torch
 from mgx import MgxEngine
 n = 65536

@@ -25,12 +25,13 @@ class EngineSource:
     """libmgx behind trajcheck's compare() protocol (raw frames recovered from
     the stacked, transposed observation)."""
 
-    def __init__(self, cfg, n_stack=4, mission_dtype=None):
+    def __init__(self, cfg, n_stack=4, mission_dtype=None, ring_depth=0, refill_every=0):
         from mgx import MgxEngine
         kw = dict(cfg)
         self.n = kw.pop("n_envs")
         self.e = MgxEngine(n_envs=self.n, n_stack=n_stack, terminal_mode="all", reward64=True,
-                           mission_dtype=mission_dtype or torch.int64, **kw)
+                           mission_dtype=mission_dtype or torch.int64, ring_depth=ring_depth,
+                           refill_every=refill_every, **kw)
         self.fs = None
 
     @staticmethod
@@ -70,6 +71,20 @@ def test_engine_matches_reference_fixture(path):
     d = dict(np.load(path))
     cfg, T = TC.fixture_cfg(d)
     src = EngineSource(cfg)
+    msg = TC.compare(src, d)
+    src.e.poll_error()
+    assert msg is None, msg
+
+
+@pytest.mark.parametrize("name", ["multi_all_s8", "multi_gtg_s8", "multi_tgl_s16", "single_pkp_s8"])
+@pytest.mark.parametrize("ring", [(-1, 0), (2, 2), (3, 1)], ids=["inline", "ring2", "ring3_every1"])
+def test_engine_reset_paths_match_fixture(name, ring):
+    """Same fixtures through the other reset paths: episodes generated inline in
+    the step kernel (no ring) and small rings refilled at different cadences."""
+    _need_gpu()
+    d = dict(np.load(TC.GOLDEN + "/traj/%s.npz" % name))
+    cfg, T = TC.fixture_cfg(d)
+    src = EngineSource(cfg, ring_depth=ring[0], refill_every=ring[1])
     msg = TC.compare(src, d)
     src.e.poll_error()
     assert msg is None, msg
