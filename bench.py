@@ -10,9 +10,12 @@ VecFrameStack(4) roll + SubprocVecEnv auto-reset, i.e. one `mgx_step`):
 
 Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel
 (mgx_step_kernel) with SURVEY.md §8(d)'s algorithmic bytes
-  B_alg = 334*steps + (3*S^2 + 208)*resets
-divided by its average launch time measured with HIP events on the launch
-stream; `traffic` is the rocprofv3 PMC figure committed under profiles/.
+  B_alg = 334*steps + (3*S^2 + 208)*resets     (per launch: one step of all N envs)
+divided by its average launch duration, measured live with HIP events on the
+launch stream around each mgx_step call that neither forks nor joins a refill
+epoch (so the event pair brackets exactly one mgx_step_kernel, which still runs
+concurrently with that epoch's refill, as in the timed region);
+`traffic` is the rocprofv3 PMC figure committed under profiles/.
 `cpu_baseline` times the C oracle (oracle/, single thread) on a bounded sample.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -48,6 +51,7 @@ def parse():
     ap.add_argument("--n-stack", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
+    ap.add_argument("--probe", type=int, default=256, help="eager steps timed per launch for the roofline")
     return ap.parse_args()
 
 
@@ -103,7 +107,8 @@ def main():
     K, W = args.steps, args.warmup
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    actions = torch.randint(0, 7, (W + K, n), device=dev, generator=g, dtype=torch.int32)
+    P = args.probe
+    actions = torch.randint(0, 7, (W + K + P, n), device=dev, generator=g, dtype=torch.int32)
     eng.reset()
     stream = torch.cuda.current_stream(dev)
     for t in range(W):
@@ -118,9 +123,9 @@ def main():
             graph.capture_begin()
             for t in range(K):
                 eng.step(actions[W + t])
+            eng.join()                      # capture must not end with the refill still forked
             graph.capture_end()
         torch.cuda.synchronize(dev)
-        # graph capture did not execute: re-seed so timed steps continue from the warmup state
     st0 = eng.stats()
     if world > 1:
         dist.barrier()
@@ -144,6 +149,21 @@ def main():
     gpu_ms = ev0.elapsed_time(ev1)
     st1 = eng.stats()
     eng.poll_error()
+    # roofline probe: per-launch duration of mgx_step_kernel (HIP events on its stream)
+    probe_us = []
+    for t in range(P):
+        if eng.epoch_boundary():
+            eng.step(actions[W + K + t])
+            continue
+        a0 = torch.cuda.Event(enable_timing=True)
+        a1 = torch.cuda.Event(enable_timing=True)
+        a0.record(stream)
+        eng.step(actions[W + K + t])
+        a1.record(stream)
+        probe_us.append((a0, a1))
+    torch.cuda.synchronize(dev)
+    eng.poll_error()
+    probe_us = [x.elapsed_time(y) * 1e3 for x, y in probe_us]
     elapsed = torch.tensor([wall, gpu_ms / 1e3], dtype=torch.float64, device=dev)
     steps_done = torch.tensor([float(st1["steps"] - st0["steps"]), float(st1["resets"] - st0["resets"])],
                               dtype=torch.float64, device=dev)
@@ -154,7 +174,7 @@ def main():
     total_env_steps, total_resets = float(steps_done[0]), float(steps_done[1])
     assert int(total_env_steps) == n * K * world, (total_env_steps, n * K * world)
     if rank == 0:
-        per_launch_s = float(gpu_ms) / 1e3 / K                       # rank-0 kernel time per launch
+        per_launch_s = (sum(probe_us) / len(probe_us)) * 1e-6 if probe_us else float(gpu_ms) / 1e3 / K
         resets_per_launch = (st1["resets"] - st0["resets"]) / K
         b_alg = B_STEP * n + (3 * args.size ** 2 + 208) * resets_per_launch
         achieved = b_alg / per_launch_s / 1e9
@@ -190,6 +210,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
                          "kernel": "mgx_step_kernel", "avg_launch_us": per_launch_s * 1e6,
+                         "probe_launches": len(probe_us),
+                         "step_pipeline_us": float(gpu_ms) * 1e3 / K,
                          "alg_bytes_per_launch": b_alg, "resets_per_launch": resets_per_launch,
                          "stack_bytes_per_launch": stack_bytes,
                          "achieved_incl_stack": (b_alg + stack_bytes) / per_launch_s / 1e9},

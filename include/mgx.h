@@ -64,6 +64,7 @@ typedef enum { MGX_TERMINAL_NONE = 0, MGX_TERMINAL_TRUNCATED = 1, MGX_TERMINAL_A
 #define MGX_DEVERR_BAD_ACTION 2u   /* action outside 0..6 (minigrid raises ValueError) */
 #define MGX_DEVERR_PCG_LOOP   4u   /* a PCG64 rejection loop exceeded its safety bound */
 #define MGX_DEVERR_OBJECTS    8u   /* generator ran out of objects (AssertionError in the reference) */
+#define MGX_DEVERR_RING_EMPTY 16u  /* an env found its episode ring empty (engine invariant broken) */
 
 typedef struct mgx_config {
     int32_t problem;           /* mgx_problem; `env.problem` */
@@ -82,8 +83,10 @@ typedef struct mgx_config {
     int32_t mission_int64;     /* 1: mission tokens int64 (TokenizeVocabWrapper dtype), 0: uint8 */
     int32_t reserved;
     int64_t mt_table_words;    /* 0 -> default (2^24); shared MT19937 output table length */
-    int32_t ring_depth;        /* pre-generated episodes per env (0 -> 64, max 255; -1 = no ring, inline resets) */
-    int32_t refill_every;      /* steps between ring refills (0 -> ring_depth; <= ring_depth) */
+    int32_t ring_depth;        /* pre-generated episodes per env (0 -> 64; rounded up to a power of two
+                                  <= 128; -1 = no ring: every auto-reset generated inline) */
+    int32_t refill_every;      /* steps per refill epoch K (0 -> ring_depth/2; clamped to <= ring_depth/2,
+                                  which guarantees the ring never runs dry: a step pops <= 1 episode) */
 } mgx_config;
 
 /* Stacked observation in the layout SB3's VecFrameStack(VecTransposeImage(.))
@@ -122,10 +125,20 @@ mgx_status mgx_destroy(mgx_handle *h);
 mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, void *stream);
 
 /* One vectorised step.  actions_dev: [N] int32 (action_bytes = 4) or int64 (8).
- * Every `refill_every` calls it also enqueues the ring refill (episode
- * pre-generation); the launch sequence depends only on the call count. */
+ * Episode pre-generation runs CONCURRENTLY with the steps on a handle-owned
+ * side stream, in epochs of K = refill_every calls: the first call of an epoch
+ * forks the refill off `stream` (after publishing the previous epoch's
+ * episodes), the last call joins it back into `stream`.  The launch sequence
+ * depends only on the call count; a stream capture (hipGraph) that covers a
+ * whole number of epochs is self-contained (else end it with mgx_join). */
 mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes,
                     const mgx_step_out *out, void *stream);
+
+/* Makes `stream` wait for the in-flight refill, if any (no host sync). */
+mgx_status mgx_join(mgx_handle *h, void *stream);
+
+/* The effective configuration (defaults resolved: ring_depth, refill_every, ...). */
+mgx_status mgx_get_config(const mgx_handle *h, mgx_config *out);
 
 /* GAE over a [T][N] f32 rollout (DictRolloutBuffer.compute_returns_and_advantage):
  * episode_starts_dev f32 [T][N], last_values f32 [N], last_dones u8 [N];

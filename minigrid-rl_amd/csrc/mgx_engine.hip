@@ -58,7 +58,10 @@ struct KParams {
     uint4 *ring_hdr;        // [N][D]   {ax|ay<<8|dir<<16|tx<<24, ty|ta<<8|mission<<16, livelocks, 0}
     uint4 *ring_rng;        // [N][D][2] RNG snapshot after that episode's generation
     uint4 *cur_rng;         // [N][2]   RNG snapshot after the current episode's generation
-    uint16_t *ring_ctl;     // [N]      head | count << 8
+    // SPSC ring indices (mod 256; D is a power of two <= 128):
+    uint8_t *ring_head;     // [N] consumer (step kernel) position
+    uint8_t *ring_tail;     // [N] producer (refill kernel) position
+    uint8_t *ring_pub;      // [N] ring_tail as of the last join: the step kernel pops below it
     uint32_t *fix_list;     // [N] envs whose ring was empty at their reset (mgx_fixup_kernel)
     uint32_t *fix_count;    // list length; fix_done: workgroups of the fixup kernel that finished
     uint32_t *fix_done;
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
         p.state[e] = st;
         store_rng(G, p, e);
         rng_snapshot(G, p.cur_rng + 2 * e);
-        p.ring_ctl[e] = 0;                               // empty ring: filled by mgx_refill_kernel
+        p.ring_head[e] = 0; p.ring_tail[e] = 0; p.ring_pub[e] = 0;   // empty ring (mgx_refill_kernel fills)
         // stacked obs: zeros + first frame
         uint8_t *row = o.img + e * (int64_t)p.img_bytes;
         for (int k = 0; k < p.img_bytes - FRAME; k++) row[k] = 0;
@@ -421,6 +424,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
 
     // ---- phase 2a: one lane per env: MiniGridEnv.step + PlaygroundEnv.step
     uint32_t my_err = 0;
+    int new_head = -1;
     bool done = false, term = false, trunc = false, dirty = false;
     int mdone = 0, rs = -1, dir = 0;
     if (tid < ne) {
@@ -549,10 +553,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
             }
             // SubprocVecEnv auto-reset: env.reset() (unseeded): pop the next pre-generated episode
             uint8_t *g = s_grid + tid * p.GSL;
-            const uint16_t ctl = p.ring_ctl[e];
-            int head = ctl & 0xFF, cnt = ctl >> 8;
-            if (cnt > 0) {
-                const int64_t slot = e * p.D + head;
+            const uint8_t head = p.D > 0 ? p.ring_head[e] : 0;
+            const bool avail = p.D > 0 && (uint8_t)(p.ring_pub[e] - head) != 0;
+            if (avail) {
+                const int64_t slot = e * p.D + (head & (p.D - 1));
                 const uint4 h = p.ring_hdr[slot];
                 const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
                 for (int c = 0; c < (p.GS >> 4); c++) {
@@ -562,8 +566,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                 }
                 p.cur_rng[2 * e] = p.ring_rng[2 * slot];
                 p.cur_rng[2 * e + 1] = p.ring_rng[2 * slot + 1];
-                head = head + 1 == p.D ? 0 : head + 1;
-                p.ring_ctl[e] = (uint16_t)(head | ((cnt - 1) << 8));
+                new_head = (int)(uint8_t)(head + 1);   // published after the barrier below, once
+                                                         // this slot's loads have been consumed
                 const int nax = h.x & 0xFF, nay = (h.x >> 8) & 0xFF, ndir = (h.x >> 16) & 0xFF;
                 const uint8_t mid = (uint8_t)(h.y >> 16);
                 EnvState ns;
@@ -580,8 +584,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                 dirty = true;
                 atomicAdd(&s_ll, (unsigned long long)h.z);
                 s_dlist[atomicAdd(&s_npop, 1)] = (uint8_t)tid;   // re-used as the render list (nd >= npop)
+            } else if (p.D > 0) {
+                // cannot happen while refill_every <= D/2 (each step pops at most one episode)
+                my_err |= MGX_DEVERR_RING_EMPTY;
             } else {
-                // empty ring: mgx_fixup_kernel generates this env's episode inline.  Keep the
+                // no ring: mgx_fixup_kernel generates this env's episode inline.  Keep the
                 // episode-spanning flags (Q2) in the state it will complete.
                 st.reward_step = (int16_t)rs; st.mission_done = (uint8_t)mdone;
                 p.state[e] = st;
@@ -595,6 +602,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     if (tid < BLOCK_ENVS) s_dirty[tid] = dirty;
     if (my_err) atomicOr(p.err, my_err);
     __syncthreads();
+    if (new_head >= 0) p.ring_head[e0 + tid] = (uint8_t)new_head;   // the refill may now reuse the slot
 #ifdef MGX_STAMPS
     ts2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -750,19 +758,19 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
     unsigned long long maxcur = 0;
     uint32_t err = 0;
     if (e < p.n) {
-        const uint16_t ctl = p.ring_ctl[e];
-        const int head = ctl & 0xFF;
-        int cnt = ctl >> 8;
-        if (cnt < p.D) {
+        // The step kernel may be popping this env's ring concurrently: `head` can be stale
+        // (older, smaller), which only under-estimates the free slots.
+        const uint8_t head = *reinterpret_cast<volatile const uint8_t *>(p.ring_head + e);
+        uint8_t tail = p.ring_tail[e];
+        int nfree = p.D - (int)(uint8_t)(tail - head);
+        if (nfree > 0) {
             Gen<NW> G;
             load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
             load_rng(G, p, e);
-            while (cnt < p.D) {
+            for (; nfree > 0; nfree--) {
                 ResetOut R;
                 reset_env(G, R);
-                int k = head + cnt;
-                if (k >= p.D) k -= p.D;
-                const int64_t slot = e * p.D + k;
+                const int64_t slot = e * p.D + (tail & (p.D - 1));
                 uint4 *dst = reinterpret_cast<uint4 *>(p.ring_grid + slot * p.GS);
                 for (int c = 0; c < (p.GS >> 4); c++) {
                     const uint32_t *q = reinterpret_cast<const uint32_t *>(G.g + c * 16);
@@ -770,10 +778,10 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
                 }
                 p.ring_hdr[slot] = pack_hdr(G, R);
                 rng_snapshot(G, p.ring_rng + 2 * slot);
-                cnt++;
+                tail++;
             }
             store_rng(G, p, e);
-            p.ring_ctl[e] = (uint16_t)(head | (cnt << 8));
+            p.ring_tail[e] = tail;                 // published to the step kernel at the next join
             maxcur = G.cur;
             err = G.err;
         }
@@ -947,7 +955,11 @@ struct mgx_handle {
     KParams kp;
     size_t lds_step, lds_reset, lds_refill;
     int nw;                 // 64-bit words of the generator's S*S cell masks (1, 2 or 4)
-    int refill_every, since_refill;
+    int refill_every;       // K: steps per refill epoch
+    uint64_t calls;         // mgx_step calls since the last mgx_reset
+    bool in_flight;         // a refill forked and not yet joined
+    hipStream_t side;       // refill stream
+    hipEvent_t ev_fork, ev_done;
     void *allocs[16];
 };
 
@@ -1010,11 +1022,18 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->device = device;
     if (h->cfg.livelock_words <= 0) h->cfg.livelock_words = MGX_LIVELOCK_WORDS;
     if (h->cfg.ring_depth == 0) h->cfg.ring_depth = 64;
-    if (h->cfg.ring_depth < 0) h->cfg.ring_depth = 0;          // ring disabled: every reset generated inline
-    if (h->cfg.ring_depth > 255) h->cfg.ring_depth = 255;
-    if (h->cfg.refill_every <= 0 || h->cfg.refill_every > h->cfg.ring_depth) h->cfg.refill_every = h->cfg.ring_depth;
+    if (h->cfg.ring_depth < 0) {
+        h->cfg.ring_depth = 0;                                   // ring disabled: every reset generated inline
+    } else {
+        int d = 2;
+        while (d < h->cfg.ring_depth && d < 128) d <<= 1;        // power of two (mod-256 ring indices)
+        h->cfg.ring_depth = d;
+    }
+    if (h->cfg.refill_every <= 0 || h->cfg.refill_every > h->cfg.ring_depth / 2)
+        h->cfg.refill_every = std::max(1, h->cfg.ring_depth / 2);
     h->refill_every = h->cfg.refill_every;
-    h->since_refill = 0;
+    h->calls = 0;
+    h->in_flight = false;
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 24;
     h->cfg.mt_table_words = (h->cfg.mt_table_words + 3) & ~(int64_t)3;
     const int64_t N = cfg->n_envs;
@@ -1037,12 +1056,12 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     }
     const int D = h->cfg.ring_depth;
     {
-        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 16, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 2};
+        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 16, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 3 + 64};
         for (int i = 0; i < 5; i++) {
             hipError_t e = hipMalloc(&h->allocs[7 + i], rs[i] ? rs[i] : 16);
             if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, std::string("hipMalloc ring: ") + hipGetErrorString(e)));
         }
-        hipError_t e = hipMemset(h->allocs[11], 0, (size_t)N * 2);
+        hipError_t e = hipMemset(h->allocs[11], 0, (size_t)N * 3 + 64);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset ring ctl"));
         e = hipMalloc(&h->allocs[12], (size_t)N * 4 + 64);
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc fix list"));
@@ -1105,7 +1124,9 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.ring_hdr = (uint4 *)h->allocs[8];
     p.ring_rng = (uint4 *)h->allocs[9];
     p.cur_rng = (uint4 *)h->allocs[10];
-    p.ring_ctl = (uint16_t *)h->allocs[11];
+    p.ring_head = (uint8_t *)h->allocs[11];
+    p.ring_tail = p.ring_head + N;
+    p.ring_pub = p.ring_head + 2 * N;
     p.fix_list = (uint32_t *)h->allocs[12];
     p.fix_count = p.fix_list + N + 4;       // 16-B aligned tail of the same allocation
     p.fix_done = p.fix_list + N + 8;
@@ -1133,6 +1154,12 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     MGX_SET_LDS(mgx_refill_kernel, h->lds_refill);
     MGX_SET_LDS(mgx_fixup_kernel, h->lds_refill);
 #undef MGX_SET_LDS
+    {
+        hipError_t e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "side stream / events"));
+    }
     (void)hipSetDevice(prev);
     *out = h;
     return MGX_OK;
@@ -1143,6 +1170,12 @@ mgx_status mgx_destroy(mgx_handle *h) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(h->device);
+    if (h->side) {
+        (void)hipStreamSynchronize(h->side);
+        (void)hipStreamDestroy(h->side);
+    }
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_done) (void)hipEventDestroy(h->ev_done);
     for (void *&p : h->allocs) if (p) { (void)hipFree(p); p = nullptr; }
     (void)hipSetDevice(prev);
     delete h;
@@ -1158,7 +1191,29 @@ static mgx_status launch_refill(mgx_handle *h, void *stream) {
         default: hipLaunchKernelGGL(mgx_refill_kernel<4>, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp); break;
     }
     HIP_TRY(hipGetLastError());
-    h->since_refill = 0;
+    return MGX_OK;
+}
+
+static mgx_status join_refill(mgx_handle *h, void *stream) {
+    if (h->in_flight) {
+        HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, h->ev_done, 0));
+        h->in_flight = false;
+    }
+    return MGX_OK;
+}
+
+// Epoch start: publish the tails the last refill reached, then fork this epoch's
+// refill onto the side stream.  It writes only slots the step kernel cannot pop
+// before the next publish, and RNG state only the refill uses.
+static mgx_status fork_refill(mgx_handle *h, void *stream) {
+    HIP_TRY(hipMemcpyAsync(h->kp.ring_pub, h->kp.ring_tail, (size_t)h->kp.n, hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+    HIP_TRY(hipEventRecord(h->ev_fork, (hipStream_t)stream));
+    HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    mgx_status s = launch_refill(h, h->side);
+    if (s != MGX_OK) return s;
+    HIP_TRY(hipEventRecord(h->ev_done, h->side));
+    h->in_flight = true;
     return MGX_OK;
 }
 
@@ -1190,6 +1245,10 @@ mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, v
         return fail(MGX_ERR_INVALID, "mgx_reset: null argument");
     KOut o = make_out(obs, nullptr);
     o.livelock = livelock_dev;
+    {
+        mgx_status js = join_refill(h, stream);  // a refill still running would race the reset
+        if (js != MGX_OK) return js;
+    }
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
     switch (h->nw) {
         case 1: hipLaunchKernelGGL(mgx_reset_kernel<1>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
@@ -1197,7 +1256,19 @@ mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, v
         default: hipLaunchKernelGGL(mgx_reset_kernel<4>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
     }
     HIP_TRY(hipGetLastError());
-    return launch_refill(h, stream);
+    h->calls = 0;
+    return launch_refill(h, stream);            // fills every ring (synchronously on `stream`)
+}
+
+mgx_status mgx_get_config(const mgx_handle *h, mgx_config *out) {
+    if (!h || !out) return fail(MGX_ERR_INVALID, "null argument");
+    *out = h->cfg;
+    return MGX_OK;
+}
+
+mgx_status mgx_join(mgx_handle *h, void *stream) {
+    if (!h) return fail(MGX_ERR_INVALID, "null handle");
+    return join_refill(h, stream);
 }
 
 mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, const mgx_step_out *out, void *stream) {
@@ -1208,19 +1279,22 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
     if (h->kp.terminal_mode != MGX_TERMINAL_NONE &&
         (!out->terminal.image_dev || !out->terminal.direction_dev || !out->terminal.mission_dev))
         return fail(MGX_ERR_INVALID, "mgx_step: terminal_mode needs terminal buffers");
+    if (action_bytes != 4 && action_bytes != 8) return fail(MGX_ERR_INVALID, "action_bytes must be 4 or 8");
     KOut o = make_out(nullptr, out);
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
+    if (h->kp.D > 0 && h->calls % (uint64_t)h->refill_every == 0) {
+        mgx_status fs = fork_refill(h, stream);
+        if (fs != MGX_OK) return fs;
+    }
     if (action_bytes == 4)
         hipLaunchKernelGGL(mgx_step_kernel<int32_t>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
                            (hipStream_t)stream, h->kp, o, (const int32_t *)actions_dev);
     else if (action_bytes == 8)
         hipLaunchKernelGGL(mgx_step_kernel<int64_t>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
                            (hipStream_t)stream, h->kp, o, (const int64_t *)actions_dev);
-    else
-        return fail(MGX_ERR_INVALID, "action_bytes must be 4 or 8");
     HIP_TRY(hipGetLastError());
-    {   // envs whose ring ran dry (every done env when the ring is disabled)
-        const unsigned fblk = h->kp.D > 0 ? (unsigned)std::min(16, h->kp.nblk) : (unsigned)h->kp.nblk;
+    if (h->kp.D == 0) {   // no ring: every done env is generated inline, right after the step
+        const unsigned fblk = (unsigned)h->kp.nblk;
         switch (h->nw) {
             case 1: hipLaunchKernelGGL(mgx_fixup_kernel<1>, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o); break;
             case 2: hipLaunchKernelGGL(mgx_fixup_kernel<2>, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o); break;
@@ -1228,7 +1302,8 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
         }
         HIP_TRY(hipGetLastError());
     }
-    if (h->kp.D > 0 && ++h->since_refill >= h->refill_every) return launch_refill(h, stream);
+    h->calls++;
+    if (h->kp.D > 0 && h->calls % (uint64_t)h->refill_every == 0) return join_refill(h, stream);
     return MGX_OK;
 }
 
@@ -1249,6 +1324,7 @@ mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const floa
 
 mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits) {
     if (!h || !bits) return fail(MGX_ERR_INVALID, "null argument");
+    HIP_TRY(hipStreamSynchronize(h->side));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     HIP_TRY(hipMemcpy(bits, h->kp.err, 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemset(h->kp.err, 0, 4));
@@ -1257,6 +1333,7 @@ mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits) {
 
 mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[4]) {
     if (!h || !out) return fail(MGX_ERR_INVALID, "null argument");
+    HIP_TRY(hipStreamSynchronize(h->side));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     unsigned long long c[8];
     HIP_TRY(hipMemcpy(c, h->kp.counters, sizeof c, hipMemcpyDeviceToHost));
@@ -1272,6 +1349,7 @@ mgx_status mgx_dump_state(mgx_handle *h, void *stream, uint8_t *grid, uint8_t *a
                           int32_t *step_count, uint8_t *mission_done, double *stored_reward, int64_t *mt_words,
                           uint64_t *pcg, uint8_t *target, uint8_t *mission_id) {
     if (!h) return fail(MGX_ERR_INVALID, "null handle");
+    HIP_TRY(hipStreamSynchronize(h->side));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     const int64_t N = h->kp.n;
     const int S = h->kp.S, GS = h->kp.GS;

@@ -17,11 +17,12 @@ MGX_OK = 0
 PROBLEMS = {"multi": 0, "full": 1, "gto": 2, "gtg": 3, "opn": 4, "pkp": 5, "drp": 6, "mov": 7}
 TERMINAL = {"none": 0, "truncated": 1, "all": 2}
 DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unknown action)",
-          4: "PCG64 rejection loop bound exceeded", 8: "object list exhausted (AssertionError)"}
+          4: "PCG64 rejection loop bound exceeded", 8: "object list exhausted (AssertionError)",
+          16: "episode ring ran dry (engine invariant broken)"}
 
 # Every entry point include/mgx.h declares (checked by tests/test_abi.py).
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
-           "mgx_gae", "mgx_poll_error", "mgx_stats", "mgx_dump_state", "mgx_mission_text")
+           "mgx_join", "mgx_get_config", "mgx_gae", "mgx_poll_error", "mgx_stats", "mgx_dump_state", "mgx_mission_text")
 
 
 class MgxConfig(ctypes.Structure):
@@ -73,6 +74,8 @@ def load():
     L.mgx_destroy.argtypes = [P]
     L.mgx_reset.argtypes = [P, ctypes.POINTER(MgxObs), P, P]
     L.mgx_step.argtypes = [P, P, I, ctypes.POINTER(MgxStepOut), P]
+    L.mgx_join.argtypes = [P, P]
+    L.mgx_get_config.argtypes = [P, ctypes.POINTER(MgxConfig)]
     L.mgx_gae.argtypes = [P, P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P]
     L.mgx_poll_error.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]
     L.mgx_stats.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64)]

@@ -62,6 +62,11 @@ class MgxEngine:
         h = _P()
         _lib.check(self.L.mgx_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)), "mgx_create")
         self.h = h
+        eff = _lib.MgxConfig()
+        _lib.check(self.L.mgx_get_config(h, ctypes.byref(eff)), "mgx_get_config")
+        self.ring_depth = int(eff.ring_depth)          # 0 = no ring (inline resets)
+        self.refill_every = int(eff.refill_every)      # K: steps per refill epoch
+        self.calls = 0                                 # mgx_step calls since the last reset()
         n, k, dev = self.n, self.n_stack, self.device
         self.obs = dict(image=torch.zeros((n, 3 * k, 7, 7), dtype=torch.uint8, device=dev),
                         direction=torch.zeros((n, 4 * k), dtype=torch.uint8, device=dev),
@@ -102,6 +107,7 @@ class MgxEngine:
         """First (seeded) reset: env i <- seed + env_index_offset + i."""
         _lib.check(self.L.mgx_reset(self.h, ctypes.byref(self._obs_c), _ptr(self.livelock), self._stream()),
                    "mgx_reset")
+        self.calls = 0
         return self.obs
 
     def step(self, actions):
@@ -112,7 +118,18 @@ class MgxEngine:
             raise ValueError("actions must be a contiguous int32/int64 [%d] tensor on %s" % (self.n, self.device))
         _lib.check(self.L.mgx_step(self.h, _ptr(actions), actions.element_size(), ctypes.byref(self._step_out),
                                    self._stream()), "mgx_step")
+        self.calls += 1
         return self.obs
+
+    def epoch_boundary(self, call=None):
+        """True if step call number `call` (default: the next one) forks or joins a refill."""
+        c = self.calls if call is None else call
+        K = self.refill_every
+        return self.ring_depth > 0 and (c % K == 0 or (c + 1) % K == 0)
+
+    def join(self):
+        """Make the current stream wait for the in-flight episode refill (mgx_join)."""
+        _lib.check(self.L.mgx_join(self.h, self._stream()), "mgx_join")
 
     def poll_error(self):
         bits = ctypes.c_uint32()

@@ -77,7 +77,7 @@ def test_engine_matches_reference_fixture(path):
 
 
 @pytest.mark.parametrize("name", ["multi_all_s8", "multi_gtg_s8", "multi_tgl_s16", "single_pkp_s8"])
-@pytest.mark.parametrize("ring", [(-1, 0), (2, 2), (3, 1)], ids=["inline", "ring2", "ring3_every1"])
+@pytest.mark.parametrize("ring", [(-1, 0), (2, 1), (4, 2), (8, 3)], ids=["inline", "ring2", "ring4", "ring8_every3"])
 def test_engine_reset_paths_match_fixture(name, ring):
     """Same fixtures through the other reset paths: episodes generated inline in
     the step kernel (no ring) and small rings refilled at different cadences."""
