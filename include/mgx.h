@@ -120,9 +120,20 @@ int mgx_abi_version(void);
 mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out);
 mgx_status mgx_destroy(mgx_handle *h);
 
-/* First (seeded) reset of every env; writes the stacked first observation
- * (zeros + newest frame).  `livelock_dev` (optional i32 [N]). */
+/* VecEnv.reset() of every env; writes the stacked first observation (zeros +
+ * newest frame).  The first call after mgx_create is the seeded reset of
+ * make_vec_env (PCG64 <- base_seed + env_index_offset + i, MT cursor 0).  Later
+ * calls follow SB3: seeded (PCG64 only) if mgx_set_seed was called since the
+ * last reset, else unseeded; both streams continue from each env's current
+ * episode, and mission_done / the stored reward persist.
+ * `livelock_dev` (optional i32 [N]). */
 mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, void *stream);
+
+/* VecEnv.seed(seed) (SB3): the NEXT mgx_reset seeds env i's PCG64 with
+ * seed + env_index_offset + i.  The MT19937 stream keeps cfg.base_seed: the
+ * reference seeds CPython `random` once, in PlaygroundEnv.__init__
+ * (custom_env.py:82), from the config, not from reset(seed). */
+mgx_status mgx_set_seed(mgx_handle *h, int64_t seed);
 
 /* One vectorised step.  actions_dev: [N] int32 (action_bytes = 4) or int64 (8).
  * Episode pre-generation runs CONCURRENTLY with the steps on a handle-owned

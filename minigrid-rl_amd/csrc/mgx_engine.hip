@@ -68,6 +68,7 @@ struct KParams {
     ulonglong4 *blk;        // [3 * nblk] per-workgroup stats: step/reset | fixup | refill workgroups
     int nblk;               // ceil(N / 64)
     int D;
+    int reset_mode;         // mgx_reset: 0 first (seeded, MT cursor 0), 1 seeded, 2 unseeded
 };
 
 struct KOut {
@@ -245,16 +246,36 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
         const int64_t e = e0 + tid;
         Gen<NW> G;
         load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
-        pcg_seed(G.pcg, (uint64_t)(p.seed_base + e));   // gymnasium Env.reset(seed=seed+i)
-        G.cur = 0;                                       // random.seed(cfg.seed) in every worker
+        EnvState st;
+        if (p.reset_mode == 0) {
+            pcg_seed(G.pcg, (uint64_t)(p.seed_base + e));   // gymnasium Env.reset(seed=seed+i)
+            G.cur = 0;                                       // random.seed(cfg.seed) in PlaygroundEnv.__init__
+            st.reward_step = -1; st.mission_done = 0;
+        } else {
+            // Later VecEnv.reset(): both streams continue from the CURRENT episode (not from the
+            // ring, which is discarded); mission_done / stored reward persist (Q2)
+            const EnvState old = p.state[e];
+            st.reward_step = old.reward_step; st.mission_done = old.mission_done;
+            const uint4 c0 = p.cur_rng[2 * e], c1 = p.cur_rng[2 * e + 1], inc = p.pcg[2 * e + 1];
+            if (p.reset_mode == 1) {
+                pcg_seed(G.pcg, (uint64_t)(p.seed_base + e));
+            } else {
+                G.pcg.sh = ((uint64_t)c0.x << 32) | c0.y;
+                G.pcg.sl = ((uint64_t)c0.z << 32) | c0.w;
+                G.pcg.ih = ((uint64_t)inc.x << 32) | inc.y;
+                G.pcg.il = ((uint64_t)inc.z << 32) | inc.w;
+                G.pcg.uinteger = c1.x;
+                G.pcg.has = c1.y;
+            }
+            G.cur = (uint64_t)c1.z | ((uint64_t)c1.w << 32);
+        }
         G.wbase = ~0ull >> 1;
         ResetOut R;
         reset_env(G, R);
-        EnvState st;
         st.ax = (uint8_t)G.ax; st.ay = (uint8_t)G.ay; st.dir = (uint8_t)G.adir; st.carry = 0;
-        st.step_count = 0; st.reward_step = -1;
+        st.step_count = 0;
         st.tx = R.tx; st.ty = R.ty; st.target_action = R.ta; st.mission_id = R.mission_id;
-        st.mission_done = 0; st.frames = 1; st.flags = 0; st.pad = 0;
+        st.frames = 1; st.flags = 0; st.pad = 0;
         p.state[e] = st;
         store_rng(G, p, e);
         rng_snapshot(G, p.cur_rng + 2 * e);
@@ -957,6 +978,8 @@ struct mgx_handle {
     int nw;                 // 64-bit words of the generator's S*S cell masks (1, 2 or 4)
     int refill_every;       // K: steps per refill epoch
     uint64_t calls;         // mgx_step calls since the last mgx_reset
+    uint64_t resets;        // mgx_reset calls since create
+    bool seed_pending;      // mgx_set_seed called since the last reset
     bool in_flight;         // a refill forked and not yet joined
     hipStream_t side;       // refill stream
     hipEvent_t ev_fork, ev_done;
@@ -1250,6 +1273,9 @@ mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, v
         if (js != MGX_OK) return js;
     }
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
+    h->kp.reset_mode = h->resets == 0 ? 0 : (h->seed_pending ? 1 : 2);
+    h->resets++;
+    h->seed_pending = false;
     switch (h->nw) {
         case 1: hipLaunchKernelGGL(mgx_reset_kernel<1>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
         case 2: hipLaunchKernelGGL(mgx_reset_kernel<2>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
@@ -1258,6 +1284,13 @@ mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, v
     HIP_TRY(hipGetLastError());
     h->calls = 0;
     return launch_refill(h, stream);            // fills every ring (synchronously on `stream`)
+}
+
+mgx_status mgx_set_seed(mgx_handle *h, int64_t seed) {
+    if (!h) return fail(MGX_ERR_INVALID, "null handle");
+    h->kp.seed_base = seed + h->cfg.env_index_offset;
+    h->seed_pending = true;
+    return MGX_OK;
 }
 
 mgx_status mgx_get_config(const mgx_handle *h, mgx_config *out) {

@@ -22,7 +22,7 @@ DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unk
 
 # Every entry point include/mgx.h declares (checked by tests/test_abi.py).
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
-           "mgx_join", "mgx_get_config", "mgx_gae", "mgx_poll_error", "mgx_stats", "mgx_dump_state", "mgx_mission_text")
+           "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_poll_error", "mgx_stats", "mgx_dump_state", "mgx_mission_text")
 
 
 class MgxConfig(ctypes.Structure):
@@ -75,6 +75,7 @@ def load():
     L.mgx_reset.argtypes = [P, ctypes.POINTER(MgxObs), P, P]
     L.mgx_step.argtypes = [P, P, I, ctypes.POINTER(MgxStepOut), P]
     L.mgx_join.argtypes = [P, P]
+    L.mgx_set_seed.argtypes = [P, I64]
     L.mgx_get_config.argtypes = [P, ctypes.POINTER(MgxConfig)]
     L.mgx_gae.argtypes = [P, P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P]
     L.mgx_poll_error.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]

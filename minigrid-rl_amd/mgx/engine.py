@@ -103,8 +103,13 @@ class MgxEngine:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    def set_seed(self, seed):
+        """VecEnv.seed: the next reset() seeds env i's PCG64 with seed + env_index_offset + i."""
+        _lib.check(self.L.mgx_set_seed(self.h, int(seed)), "mgx_set_seed")
+        self.seed = int(seed)
+
     def reset(self):
-        """First (seeded) reset: env i <- seed + env_index_offset + i."""
+        """Seeded reset of every env: env i <- seed + env_index_offset + i (MT cursor 0)."""
         _lib.check(self.L.mgx_reset(self.h, ctypes.byref(self._obs_c), _ptr(self.livelock), self._stream()),
                    "mgx_reset")
         self.calls = 0

@@ -864,17 +864,24 @@ static void emit_obs(env_t *e, int i, uint8_t *img_src, uint8_t *img, uint8_t *d
     if (mis) tokenize(e->mission, mis + (size_t)i * 32);
 }
 
-/* First (seeded) reset of every env: env i gets seed base_seed + index_offset + i. */
-EXPORT void orc_reset(orc_vec *v, int64_t base_seed, int64_t index_offset,
-                      uint8_t *img, uint8_t *dir, uint8_t *mis, int32_t *livelock) {
+/* VecEnv.reset() of every env.  seeded: env i gets seed base_seed + index_offset + i
+ * (SB3 VecEnv.seed / make_vec_env); unseeded: both streams continue.  The MT19937
+ * stream is never re-seeded (random.seed runs once, in PlaygroundEnv.__init__). */
+EXPORT void orc_reset_ex(orc_vec *v, int seeded, int64_t base_seed, int64_t index_offset,
+                         uint8_t *img, uint8_t *dir, uint8_t *mis, int32_t *livelock) {
     for (int i = 0; i < v->n; i++) {
         env_t *e = &v->e[i];
-        int nll = env_reset(e, 1, (uint64_t)(base_seed + index_offset + i));
+        int nll = env_reset(e, seeded, (uint64_t)(base_seed + index_offset + i));
         uint8_t im[7][7][3];
         gen_obs(e, im);
         emit_obs(e, i, &im[0][0][0], img, dir, mis);
         if (livelock) livelock[i] = nll;
     }
+}
+
+EXPORT void orc_reset(orc_vec *v, int64_t base_seed, int64_t index_offset,
+                      uint8_t *img, uint8_t *dir, uint8_t *mis, int32_t *livelock) {
+    orc_reset_ex(v, 1, base_seed, index_offset, img, dir, mis, livelock);
 }
 
 /* One vectorised step with SubprocVecEnv auto-reset.  Outputs (NULL = skip):

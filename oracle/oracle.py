@@ -45,6 +45,7 @@ def lib():
         L.orc_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
         L.orc_destroy.argtypes = [P]
         L.orc_reset.argtypes = [P, ctypes.c_int64, ctypes.c_int64, P, P, P, P]
+        L.orc_reset_ex.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, P, P, P, P]
         L.orc_step.argtypes = [P] * 12
         L.orc_dump.argtypes = [P] * 10
         L.orc_mission.restype = ctypes.c_char_p
@@ -85,10 +86,13 @@ class OracleVec:
         n = self.n
         return (np.zeros((n, 7, 7, 3), np.uint8), np.zeros(n, np.uint8), np.zeros((n, 32), np.uint8))
 
-    def reset(self):
+    def reset(self, seed="init"):
+        """VecEnv.reset(): seed="init" -> the configured seed; an int -> that seed
+        (after VecEnv.seed); None -> unseeded (streams continue)."""
         img, d, m = self._obs_bufs()
         ll = np.zeros(self.n, np.int32)
-        self.L.orc_reset(self.h, self.seed, self.offset, _p(img), _p(d), _p(m), _p(ll))
+        sd = self.seed if seed == "init" else (0 if seed is None else int(seed))
+        self.L.orc_reset_ex(self.h, int(seed is not None), sd, self.offset, _p(img), _p(d), _p(m), _p(ll))
         return dict(image=img, dir=d, mission=m, livelock=ll)
 
     def step(self, actions):

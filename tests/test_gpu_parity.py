@@ -227,3 +227,29 @@ def test_baseline_size_properties():
     st = e1.stats()
     assert st["steps"] == n * T and st["resets"] > n
     e1.poll_error()
+
+
+def test_sharded_engines_equal_one_engine():
+    """Env sharding: two handles owning global envs [0, n) and
+    [n, 2n) (env_index_offset) step exactly like one handle owning [0, 2n)."""
+    _need_gpu()
+    from mgx import MgxEngine
+    n, T = 4096, 96
+    whole = MgxEngine(problem="multi", mission=None, size=8, n_envs=2 * n)
+    parts = [MgxEngine(problem="multi", mission=None, size=8, n_envs=n, env_index_offset=r * n) for r in range(2)]
+    whole.reset()
+    for p in parts:
+        p.reset()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    for t in range(T):
+        a = torch.randint(0, 7, (2 * n,), device="cuda", generator=g)
+        ow = whole.step(a)
+        op = [p.step(a[r * n:(r + 1) * n].contiguous()) for r, p in enumerate(parts)]
+        for k in ow:
+            assert torch.equal(ow[k], torch.cat([o[k] for o in op])), (t, k)
+        assert torch.equal(whole.reward, torch.cat([p.reward for p in parts])), t
+    sw = whole.stats()
+    sp = [p.stats() for p in parts]
+    assert sw["resets"] == sum(s["resets"] for s in sp)
+    whole.poll_error()

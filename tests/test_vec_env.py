@@ -1,0 +1,96 @@
+"""MgxVecEnv (the SB3 VecEnv drop-in, mgx/vec_env.py) against a VecEnv built
+from the C oracle + the numpy SB3 layer: obs, rewards, dones and every info
+field (terminal_observation, TimeLimit.truncated, Monitor episode r/l), plus
+SB3's reset semantics (first reset seeded, later resets unseeded unless
+VecEnv.seed() was called; mission_done / stored reward persist, Q2)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+class OracleVecEnv:
+    """SubprocVecEnv(Monitor(make_env)) + VecTransposeImage + VecFrameStack, restated."""
+
+    def __init__(self, n, n_stack, **kw):
+        import oracle as O
+        self.O = O
+        self.v = O.OracleVec(n_envs=n, **kw)
+        self.fs = O.FrameStackOracle(n, n_stack)
+        self.n = n
+        self.ep_len = np.zeros(n, np.int64)
+
+    def _raw(self, img, d, m):
+        O = self.O
+        return dict(image=O.vec_transpose_image(img), direction=O.one_hot_dir(d), mission=m.astype(np.int64))
+
+    def reset(self, seed="init"):
+        r = self.v.reset(seed)
+        self.ep_len[:] = 0
+        return self.fs.reset(self._raw(r["image"], r["dir"], r["mission"]))
+
+    def step(self, actions):
+        o = self.v.step(actions)
+        done = (o["terminated"] | o["truncated"]).astype(bool)
+        self.ep_len += 1
+        cur = self._raw(np.where(done[:, None, None, None], o["r_image"], o["image"]),
+                        np.where(done, o["r_dir"], o["dir"]), np.where(done[:, None], o["r_mission"], o["mission"]))
+        obs, term = self.fs.step(cur, done, self._raw(o["image"], o["dir"], o["mission"]))
+        infos = [{} for _ in range(self.n)]
+        for i in np.nonzero(done)[0]:
+            infos[i] = {"TimeLimit.truncated": bool(o["truncated"][i] and not o["terminated"][i]),
+                        "terminal_observation": {k: v[i] for k, v in term.items()},
+                        "episode": {"r": round(float(o["reward"][i]), 6), "l": int(self.ep_len[i])}}
+        self.ep_len[done] = 0
+        return obs, o["reward"].astype(np.float32), done, infos
+
+
+def _same_obs(a, b):
+    return all(np.array_equal(np.asarray(a[k]).astype(np.int64), np.asarray(b[k]).astype(np.int64)) for k in b)
+
+
+@pytest.mark.parametrize("problem,mission,size,n_stack", [("multi", 5, 8, 4), ("multi", None, 11, 4),
+                                                          ("pkp", 2, 8, 3)])
+def test_vec_env_matches_sb3_stack(problem, mission, size, n_stack):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mgx import MgxVecEnv
+    n, T = 256, 160
+    kw = dict(problem=problem, mission=mission, size=size, num_objects=4, seed=42)
+    ref = OracleVecEnv(n, n_stack, **kw)
+    env = MgxVecEnv(n, n_frames_stack=n_stack, **kw)
+    assert env.num_envs == n and env.action_space.n == 7
+    assert env.observation_space["image"].shape == (3 * n_stack, 7, 7)
+    rng = np.random.default_rng(17)
+
+    def run(steps):
+        for t in range(steps):
+            a = rng.integers(0, 7, n)
+            o1, r1, d1, i1 = env.step(a)
+            o2, r2, d2, i2 = ref.step(a.astype(np.int32))
+            assert _same_obs(o1, o2), t
+            assert np.array_equal(r1, r2) and r1.dtype == np.float32, t
+            assert np.array_equal(d1, d2) and d1.dtype == bool, t
+            for i in np.nonzero(d2)[0]:
+                assert i1[i]["TimeLimit.truncated"] == i2[i]["TimeLimit.truncated"], (t, i)
+                assert _same_obs(i1[i]["terminal_observation"], i2[i]["terminal_observation"]), (t, i)
+                assert i1[i]["episode"]["r"] == i2[i]["episode"]["r"], (t, i)
+                assert i1[i]["episode"]["l"] == i2[i]["episode"]["l"], (t, i)
+            assert all(not x for j, x in enumerate(i1) if not d1[j])
+
+    assert _same_obs(env.reset(), ref.reset())
+    run(T)
+    # a later VecEnv.reset() is unseeded: both streams continue from the current episode
+    assert _same_obs(env.reset(), ref.reset(None))
+    run(40)
+    # VecEnv.seed(s) -> the next reset re-seeds PCG64 with s + i; MT continues
+    seeds = env.seed(1000)
+    assert seeds[:2] == [1000, 1001]
+    assert _same_obs(env.reset(), ref.reset(1000))
+    run(40)
+    a, b = env.engine.dump_state(), ref.v.dump()
+    for k in ("grid", "agent", "mission_done", "mtwords", "pcg"):
+        assert np.array_equal(a[k], b[k]), k
+    env.close()
