@@ -20,6 +20,11 @@ concurrently with that epoch's refill, as in the timed region);
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+
+  python bench.py --workload ppo [--steps K] [--warmup W]
+  BASELINE config 3: the full PPO loop (PKP 8x8, 65,536 envs/GPU, PyTorch policy,
+  device-resident rollout + train); a "step" is one PPO iteration (collect
+  `--horizon` env steps + n_epochs of minibatch training); value = env-steps/s.
 """
 import argparse
 import json
@@ -52,6 +57,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
     ap.add_argument("--probe", type=int, default=256, help="eager steps timed per launch for the roofline")
+    ap.add_argument("--workload", default="rollout", choices=["rollout", "ppo"])
+    ap.add_argument("--horizon", type=int, default=16, help="ppo: env steps per rollout")
+    ap.add_argument("--batch-size", type=int, default=16384, help="ppo: minibatch size")
+    ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
     return ap.parse_args()
 
 
@@ -88,6 +97,80 @@ def _cpu_model():
     return "unknown"
 
 
+def main_ppo(args, world, rank, local, dev):
+    """BASELINE config 3: PPO(CustomPPOPolicy) on PKP 8x8 with the engine (mgx/ppo.py)."""
+    from mgx.policy import ActorCriticPolicy
+    from mgx.ppo import PPOConfig, RolloutCollector, Trainer
+    from mgx import MgxEngine
+    mission = None if args.mission == "None" else int(args.mission)
+    if args.mission == "5" and args.problem == "multi":
+        mission = 2                                   # config 3 is PKP ('pick up')
+    n = args.n_envs
+    cfg = PPOConfig(n_envs=n, horizon=args.horizon, batch_size=args.batch_size, n_epochs=args.epochs,
+                    env=dict(problem=args.problem, mission=mission, size=args.size, num_objects=4))
+    torch.manual_seed(cfg.seed + rank)
+    eng = MgxEngine(n_envs=n, seed=cfg.seed, env_index_offset=rank * n, n_stack=cfg.n_frames_stack,
+                    terminal_mode="truncated", mission_dtype=torch.uint8, device=dev, **cfg.env)
+    pol = ActorCriticPolicy(n_stack=cfg.n_frames_stack, optim_eps=cfg.optim_eps, lr=cfg.initial_learning_rate,
+                            mission_cache=cfg.mission_cache).to(dev)
+    group = dist.group.WORLD if world > 1 else None
+    if group is not None:
+        for p_ in pol.parameters():
+            dist.broadcast(p_.data, 0)
+    col = RolloutCollector(eng, pol, cfg)
+    tr = Trainer(pol, cfg, group)
+    col.start()
+    K, W = args.steps, args.warmup
+    total = (K + W) * n * cfg.horizon * world
+
+    def iteration():
+        t0 = time.perf_counter()
+        buf = col.collect()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        tr.global_adv_stats(buf)
+        tr.train(buf, 1.0 - float(col.num_timesteps * world) / total)
+        torch.cuda.synchronize(dev)
+        return t1 - t0, time.perf_counter() - t1
+
+    for _ in range(W):
+        iteration()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    tc = tt = 0.0
+    for _ in range(K):
+        a, b = iteration()
+        tc += a
+        tt += b
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+    eng.poll_error()
+    wall = float(wall[0])
+    if rank == 0:
+        print(json.dumps({
+            "metric": "PPO env-steps/sec (rollout + train), PKP 8x8, 65k envs/GPU",
+            "value": K * n * cfg.horizon * world / wall, "unit": "env-steps/s", "n_gpus": world, "steps": K,
+            "warmup": W, "ms_per_step": wall * 1e3 / K, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8 env / fp32 policy",
+            "data": "synthetic (policy-sampled actions; env i seeded 42+i; random-init policy)",
+            "config": {"workload": "PKP 8x8 full PPO loop, %d envs/GPU (BASELINE config 3)" % n,
+                       "problem": args.problem, "mission": mission, "size": args.size, "envs_per_gpu": n,
+                       "horizon": cfg.horizon, "batch_size": cfg.batch_size, "n_epochs": cfg.n_epochs,
+                       "minibatches_per_epoch": n * world * cfg.horizon // cfg.batch_size // world,
+                       "mission_cache": cfg.mission_cache, "parallelism": "env-sharded dp%d" % world},
+            "phases_s_per_iter": {"collect": tc / K, "train": tt / K},
+            "roofline": None,
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -98,6 +181,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.workload == "ppo":
+        return main_ppo(args, world, rank, local, dev)
     from mgx import MgxEngine
 
     n = args.n_envs
