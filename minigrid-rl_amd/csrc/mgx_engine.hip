@@ -135,6 +135,22 @@ __device__ __forceinline__ void write_mission_slot(void *mis, int mission64, int
     }
 }
 
+// One 16-B chunk of slot `s` of env e's mission stack: tokens (2 int64 or 16 u8 per
+// chunk) or zeros.  Used by the step kernel's block-cooperative writer, so that one
+// env's 1-KB (int64) stack row is written by consecutive threads, coalesced.
+__device__ __forceinline__ void write_mission_chunk(void *mis, int mission64, int64_t e, int n_stack, int s, int c,
+                                                    const uint8_t *tok /* null = zeros */) {
+    if (mission64) {
+        longlong2 v = make_longlong2(0, 0);
+        if (tok) { v.x = tok[2 * c]; v.y = tok[2 * c + 1]; }
+        reinterpret_cast<longlong2 *>(reinterpret_cast<int64_t *>(mis) + (e * n_stack + s) * 32)[c] = v;
+    } else {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (tok) v = reinterpret_cast<const uint4 *>(tok)[c];
+        reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(mis) + (e * n_stack + s) * 32)[c] = v;
+    }
+}
+
 // Full mission stack for an episode holding `frames` frames (last `frames` slots set).
 __device__ __forceinline__ void write_mission_stack(void *mis, int mission64, int64_t e, int n_stack, int frames,
                                                     const uint8_t *tok) {
@@ -364,25 +380,33 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params ax | ay<<8 | dir<<16 | carry<<24
     __shared__ uint8_t s_done[BLOCK_ENVS];
     __shared__ uint8_t s_dirty[BLOCK_ENVS];
-    __shared__ uint8_t s_dlist[BLOCK_ENVS];
-    __shared__ int s_nd, s_npop;
+    __shared__ uint8_t s_dlist[BLOCK_ENVS];      // envs that popped a new episode (render + mission lists)
+    __shared__ uint8_t s_flist[BLOCK_ENVS];      // envs whose mission stack is still filling
+    __shared__ uint8_t s_fslot[BLOCK_ENVS];      // ... and the slot that flips 0 -> tokens
+    __shared__ uint8_t s_mid[BLOCK_ENVS];        // mission id whose tokens those writes use
+    __shared__ int s_nd, s_npop, s_nf;
     __shared__ unsigned long long s_ll;
 
     const int tid = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * BLOCK_ENVS;
     const int ne = (int)min<int64_t>(BLOCK_ENVS, p.n - e0);
     const int S = p.S;
-    if (tid == 0) { s_nd = 0; s_npop = 0; s_ll = 0; }
+    if (tid == 0) s_ll = 0;
 #ifdef MGX_STAMPS
     const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-    unsigned long long ts1 = 0, ts2 = 0;
+    unsigned long long ts1 = 0, ts2 = 0, tsA = 0, tsB = 0;
 #endif
 
     // ---- phase 1: issue every independent load up front --------------------------
     // (a) this lane's env state + action (wave 0)
     EnvState st;
     int a = 0;
-    if (tid < ne) { st = p.state[e0 + tid]; a = (int)actions[e0 + tid]; }
+    uint4 odir = make_uint4(0, 0, 0, 0);          // old direction stack (n_stack == 4: one uint4)
+    if (tid < ne) {
+        st = p.state[e0 + tid];
+        a = (int)actions[e0 + tid];
+        if (p.n_stack == 4) odir = reinterpret_cast<const uint4 *>(o.dir)[e0 + tid];
+    }
     // (b) fast roll: the old image-stack dwords this lane's output quads need, into registers
     constexpr int DW = FRAME_DW4;                                                     // 147
     constexpr int MAXQ = (BLOCK_ENVS * DW / 4 + BLOCK_THREADS - 1) / BLOCK_THREADS;  // 10
@@ -446,7 +470,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     // ---- phase 2a: one lane per env: MiniGridEnv.step + PlaygroundEnv.step
     uint32_t my_err = 0;
     int new_head = -1;
-    bool done = false, term = false, trunc = false, dirty = false;
+    bool done = false, term = false, trunc = false, dirty = false, fill = false, popped = false;
     int mdone = 0, rs = -1, dir = 0;
     if (tid < ne) {
         const int64_t e = e0 + tid;
@@ -535,26 +559,41 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         if (o.ep_len) o.ep_len[e] = sc;
         if (!done) {
             const int frames = min((int)st.frames + 1, p.n_stack);
-            dir_stack_roll(o.dir, o.dir, e, p.n_stack, dir);
-            if (st.frames < p.n_stack)                 // stack still filling: one slot flips 0 -> mission
-                write_mission_slot(o.mis, p.mission64, e, p.n_stack, p.n_stack - frames, p.mtok + st.mission_id * 32);
+            if (p.n_stack == 4)
+                reinterpret_cast<uint4 *>(o.dir)[e] = make_uint4(odir.y, odir.z, odir.w, 1u << (8 * dir));
+            else
+                dir_stack_roll(o.dir, o.dir, e, p.n_stack, dir);
+            if (st.frames < p.n_stack) {               // stack still filling: one slot flips 0 -> mission
+                fill = true;
+                s_fslot[tid] = (uint8_t)(p.n_stack - frames);
+                s_mid[tid] = st.mission_id;
+            }
             st.ax = (uint8_t)ax; st.ay = (uint8_t)ay; st.dir = (uint8_t)dir; st.carry = carry;
             st.step_count = (uint16_t)sc; st.reward_step = (int16_t)rs; st.mission_done = (uint8_t)mdone;
             st.frames = (uint8_t)frames;
             p.state[e] = st;
             if (o.livelock) o.livelock[e] = 0;
-        } else {
-            s_dlist[atomicAdd(&s_nd, 1)] = (uint8_t)tid;
         }
         s_done[tid] = done;
     } else if (tid < BLOCK_ENVS) {
         s_done[tid] = 0;
     }
+    if (tid < BLOCK_ENVS) {                            // wave 0: ballot compaction of the fill list
+        const unsigned long long fm = __ballot(fill), dm = __ballot(done);
+        if (fill) s_flist[__popcll(fm & __lanemask_lt())] = (uint8_t)tid;
+        if (tid == 0) { s_nf = __popcll(fm); s_nd = __popcll(dm); }
+    }
     __syncthreads();
 
+#ifdef MGX_STAMPS
+    tsA = __builtin_amdgcn_s_memtime();
+#endif
     // ---- phase 2b: render every env's frame (all 256 threads)
     render_block(s_grid, s_stk, s_rp, nullptr, ne, S, p.GSL, FSTRIDE, FOFF);
     __syncthreads();
+#ifdef MGX_STAMPS
+    tsB = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- phase 2c: done envs: terminal_observation, then auto-reset from the ring
     const int nd = s_nd;
@@ -569,7 +608,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                 const uint8_t *old = fast ? o.img + e * (int64_t)IMG : s_stk + tid * IMG;
                 for (int off = 0; off < IMG - FRAME; off++) t[off] = old[off + FRAME];
                 for (int k = 0; k < FRAME; k++) t[IMG - FRAME + k] = fr[k];
-                dir_stack_roll(o.dir, o.t_dir, e, p.n_stack, dir);
+                if (p.n_stack == 4)
+                    reinterpret_cast<uint4 *>(o.t_dir)[e] = make_uint4(odir.y, odir.z, odir.w, 1u << (8 * dir));
+                else
+                    dir_stack_roll(o.dir, o.t_dir, e, p.n_stack, dir);
                 write_mission_stack(o.t_mis, p.mission64, e, p.n_stack, frames, p.mtok + st.mission_id * 32);
             }
             // SubprocVecEnv auto-reset: env.reset() (unseeded): pop the next pre-generated episode
@@ -600,11 +642,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                 p.state[e] = ns;
                 s_rp[tid] = (uint32_t)nax | ((uint32_t)nay << 8) | ((uint32_t)ndir << 16);
                 dir_stack_fresh(o.dir, e, p.n_stack, ndir);
-                write_mission_stack(o.mis, p.mission64, e, p.n_stack, 1, p.mtok + mid * 32);
+                s_mid[tid] = mid;                                 // fresh mission stack: block writer below
                 if (o.livelock) o.livelock[e] = (int)h.z;
                 dirty = true;
-                atomicAdd(&s_ll, (unsigned long long)h.z);
-                s_dlist[atomicAdd(&s_npop, 1)] = (uint8_t)tid;   // re-used as the render list (nd >= npop)
+                popped = true;
+                if (h.z) atomicAdd(&s_ll, (unsigned long long)h.z);
             } else if (p.D > 0) {
                 // cannot happen while refill_every <= D/2 (each step pops at most one episode)
                 my_err |= MGX_DEVERR_RING_EMPTY;
@@ -616,9 +658,34 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                 p.fix_list[atomicAdd(p.fix_count, 1u)] = (uint32_t)e;
             }
         }
+        if (tid < BLOCK_ENVS) {                        // wave 0: ballot compaction of the pop list
+            const unsigned long long pm = __ballot(popped);
+            if (popped) s_dlist[__popcll(pm & __lanemask_lt())] = (uint8_t)tid;
+            if (tid == 0) s_npop = __popcll(pm);
+        }
         __syncthreads();
         // first frames of the new episodes -> frame rows (phase 3 zero-fills the older slots)
         render_block(s_grid, s_stk, s_rp, s_dlist, s_npop, S, p.GSL, FSTRIDE, FOFF);
+    } else if (tid == 0) {
+        s_npop = 0;
+    }
+    __syncthreads();
+    // mission stacks, block-cooperative and coalesced: fresh stacks of popped envs
+    // (zeros + tokens in the newest slot), then the one flipping slot of filling envs
+    {
+        const int K = p.n_stack, CPS = p.mission64 ? 16 : 2, per = K * CPS;
+        const int tot_d = s_npop * per;
+        for (int w = tid; w < tot_d; w += BLOCK_THREADS) {
+            const int i = w / per, j = w - i * per;
+            const int le = s_dlist[i], sl = j / CPS, c = j - sl * CPS;
+            write_mission_chunk(o.mis, p.mission64, e0 + le, K, sl, c, sl == K - 1 ? p.mtok + s_mid[le] * 32 : nullptr);
+        }
+        const int tot_f = s_nf * CPS;
+        for (int w = tid; w < tot_f; w += BLOCK_THREADS) {
+            const int i = w / CPS, c = w - i * CPS;
+            const int le = s_flist[i];
+            write_mission_chunk(o.mis, p.mission64, e0 + le, K, s_fslot[le], c, p.mtok + s_mid[le] * 32);
+        }
     }
     if (tid < BLOCK_ENVS) s_dirty[tid] = dirty;
     if (my_err) atomicOr(p.err, my_err);
@@ -687,14 +754,20 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     // ---- phase 5: write back grids that changed (moves, pickups, resets)
     grid_copy_out(p.grid + e0 * p.GS, s_grid, ne, p.GS, p.GSL, s_dirty);
     if (tid == 0) {
-        ulonglong4 b = p.blk[blockIdx.x];           // workgroup-private stats slot (no contention)
-        b.x += (unsigned long long)ne; b.y += (unsigned long long)nd; b.z += s_ll;
-        p.blk[blockIdx.x] = b;
+        // workgroup-private stats slot: fire-and-forget adds (no load on the kernel's tail)
+        atomicAdd(&p.blk[blockIdx.x].x, (unsigned long long)ne);
+        if (nd) atomicAdd(&p.blk[blockIdx.x].y, (unsigned long long)nd);
+        if (s_ll) atomicAdd(&p.blk[blockIdx.x].z, s_ll);
 #ifdef MGX_STAMPS
         const unsigned long long ts4 = __builtin_amdgcn_s_memtime();
         atomicAdd(&p.counters[4], ts1 - ts0);   // phase 1: loads
-        atomicAdd(&p.counters[5], ts2 - ts1);   // phase 2: step + render + resets
-        atomicAdd(&p.counters[6], ts4 - ts2);   // phase 3+5: stack + grid write-back
+        atomicAdd(&p.counters[5], tsA - ts1);   // phase 2a: step logic
+#if MGX_STAMPS == 2
+        atomicAdd(&p.counters[6], tsB - tsA);   // phase 2b: render
+#else
+        atomicAdd(&p.counters[6], ts2 - tsA);   // phase 2b+2c: render, done envs, ring pops, render
+#endif
+        atomicAdd(&p.counters[7], ts4 - ts2);   // phase 3+5: stack roll + grid write-back
 #endif
     }
 }

@@ -3,6 +3,7 @@ import os; sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.
 import torch
 from mgx import MgxEngine
 n = 65536
+import sys as _s
 e = MgxEngine(problem="multi", mission=5, size=8, n_envs=n)
 acts = torch.randint(0, 7, (256, n), device="cuda", dtype=torch.int32)
 torch.cuda.synchronize(); t=time.perf_counter()

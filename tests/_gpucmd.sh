@@ -6,8 +6,10 @@ R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 timeout -k 10 600 python -m pytest tests -m gpu -q -x -rf > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
-MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_stamps.so timeout -k 10 200 python tests/_diag_phases.py > gpurun_out/diag.log 2>&1
-tail -3 gpurun_out/diag.log
+for v in "" 2; do
+  MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_stamps$v.so timeout -k 10 200 python tests/_diag_phases.py > gpurun_out/diag$v.log 2>&1
+  tail -1 gpurun_out/diag$v.log
+done
 timeout -k 10 300 python bench.py --steps 2048 --warmup 128 --cpu-seconds 0 > gpurun_out/bench.json 2>gpurun_out/bench.err
 cat gpurun_out/bench.json
 cd /tmp && export TMPDIR=/tmp
