@@ -169,6 +169,10 @@ mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits);
  * Synchronises `stream`. */
 mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]);
 
+/* Diagnostics: the first n (<= 32) raw device counters (phase / section clocks of
+ * -DMGX_STAMPS / -DMGX_GEN_STAMPS builds; zero otherwise).  Synchronises. */
+mgx_status mgx_debug_counters(mgx_handle *h, void *stream, uint64_t *out, int n);
+
 /* Test/debug: copy env state to HOST buffers (any may be NULL); synchronises.
  * grid u8 [N][S][S][4] (x-major (type,colour,state,box-holds-key)), agent u8 [N][3],
  * carrying u8 [N][4], step_count i32 [N], mission_done u8 [N], stored_reward f64 [N]

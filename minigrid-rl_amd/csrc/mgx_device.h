@@ -206,8 +206,16 @@ __device__ __forceinline__ void pcg_seed(Pcg &p, uint64_t seed) {
 // door-adjacency as S*S-bit masks (NW 64-bit words), the next four MT19937
 // words in a register queue -- and only WRITES the cell codes to the LDS grid
 // row (read back once, when the finished grid is copied out).
-constexpr int MT_WIN = 64;        // words per lane-private LDS window
-constexpr int WIN_STRIDE = 65;    // words per lane window (odd -> lane-private rows hit distinct banks)
+// MT19937 words are consumed ONLY through random._randbelow(n) with n < 32, which
+// reads just the top k = bit_length(n) <= 5 bits of each word.  The engine therefore
+// keeps the shared MT(seed) output stream as 5-bit fields, ten per u64 group (6-bit
+// slots, bit 5 of every slot a zero guard): 5x denser than the words, and a SWAR
+// compare tests ten candidate words at once (see randbelow).
+constexpr int MT_FIELDS = 10;       // words per packed group
+constexpr int MT_WG = 32;           // groups per lane-private LDS window (320 words)
+constexpr int WIN_STRIDE = 66;      // dwords per lane window row: 8-B aligned, 2-way banked for b64
+constexpr uint64_t MT_REP = 0x041041041041041ull;   // 1 in every 6-bit slot of ten
+constexpr uint64_t MT_LOW60 = (1ull << 60) - 1ull;
 constexpr int MAX_OBJS = 32;
 constexpr int OBJ_STRIDE = 33;    // words per lane objs list (odd, same reason)
 constexpr int SAT_PROBE = 64;     // rejections before the exhaustive satisfiability probe
@@ -256,11 +264,13 @@ struct Gen {
     Bits<NW> occ;          // cell holds an object (walls, doors, goal, keys, boxes, balls)
     Bits<NW> dn;           // cell is next to a door (custom_env.py:2036-2046)
     // MT19937 shared table + cursor: q0..q3 = table[cur .. cur+3]
-    const uint32_t *table;
-    uint64_t tlen;
-    uint32_t *win;         // LDS window (MT_WIN words) = table[wbase .. wbase + MT_WIN)
-    uint64_t wbase, cur, astart;
-    uint32_t q0, q1, q2, q3;
+    const uint64_t *table; // packed MT19937 field groups (global)
+    uint64_t tlen;         // groups in the table
+    uint64_t *win;         // LDS window: packed groups [gbase, gbase + MT_WG)
+    uint64_t gbase;        // first group in the window
+    uint64_t cur, astart;  // word cursor; first word of the current reset attempt
+    uint64_t ga, gb, gc;   // packed groups g, g+1 (ready), g+2 (LDS read in flight), g = cur / 10
+    int go;                // cur % 10
     uint32_t llw;
     bool abort;
     uint32_t err;
@@ -268,9 +278,34 @@ struct Gen {
     int ax, ay, adir;
     uint32_t *objs;        // LDS objs list: type | cname<<4 | x<<8 | y<<16 (cname 15 = None)
     int nobjs;
+    uint32_t tmask;        // bit t: an object of type t is in objs
     // config
     int problem, cfg_mission, num_objects, all_doors_open;
+#ifdef MGX_GEN_STAMPS
+    unsigned long long *stamps;   // diagnostic build: per-section wave clocks (counters[8..])
+    uint64_t tlast;
+#endif
 };
+
+// Diagnostic section clock (MGX_GEN_STAMPS builds only): the first active lane of
+// the wave adds the shader clocks since this lane's previous stamp to counter k.
+#ifdef MGX_GEN_STAMPS
+#define GSTAMP(G, k)                                                                     \
+    do {                                                                                 \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();                                \
+        const unsigned long long _m = __ballot(1);                                       \
+        if ((int)__lane_id() == __ffsll((long long)_m) - 1) atomicAdd(&(G).stamps[k], _t - (G).tlast); \
+        (G).tlast = _t;                                                                  \
+    } while (0)
+#define GCOUNT(G, k)                                                                     \
+    do {                                                                                 \
+        const unsigned long long _m = __ballot(1);                                       \
+        if ((int)__lane_id() == __ffsll((long long)_m) - 1) atomicAdd(&(G).stamps[k], 1ull); \
+    } while (0)
+#else
+#define GSTAMP(G, k) do { } while (0)
+#define GCOUNT(G, k) do { } while (0)
+#endif
 
 template <int NW>
 __device__ __forceinline__ void put(Gen<NW> &G, int x, int y, uint8_t code) {   // grid.set(x, y, obj)
@@ -279,63 +314,84 @@ __device__ __forceinline__ void put(Gen<NW> &G, int x, int y, uint8_t code) {   
     if (code == CODE_EMPTY) G.occ.unset(b); else G.occ.set(b);
 }
 
-// Refill the lane's LDS window with table[from & ~3 .. +MT_WIN): 16 independent
-// 16-B global loads in flight (one L2/HBM round trip), 64 dword LDS stores
-// (the window row is 4-B aligned: odd dword stride avoids bank conflicts).
-__device__ __forceinline__ uint64_t mt_refill(const uint32_t *__restrict__ table, uint64_t tlen, uint32_t *win,
-                                              uint64_t from, uint32_t &err) {
-    uint64_t base = from & ~3ull;
-    if (base + MT_WIN > tlen) { err |= 1u; base = tlen; }   // MGX_DEVERR_MT_TABLE: read the zero pad
+// Refill the lane's LDS window with packed groups [g, g + MT_WG): 16 independent
+// 16-B global loads in flight (one L2/HBM round trip), 32 b64 LDS stores.
+// Out of line: it is the cold path of every draw site (inlined at each of them it
+// made the generator ~2k instructions larger).  Returns ngroups when the table ran out.
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+__device__ __noinline__ uint64_t mt_refill_cold(const uint64_t *__restrict__ table, uint64_t ngroups, lds_u64 *win,
+                                                uint64_t g) {
+    uint64_t base = g;
+    if (base + MT_WG > ngroups) base = ngroups;          // MGX_DEVERR_MT_TABLE: read the zero pad
     const uint4 *src = reinterpret_cast<const uint4 *>(table + base);
 #pragma unroll
-    for (int h = 0; h < MT_WIN / 16; h++) {        // 4 x (4 loads in flight, then 16 LDS stores)
-        uint4 v0 = src[4 * h], v1 = src[4 * h + 1], v2 = src[4 * h + 2], v3 = src[4 * h + 3];
-        uint32_t *d = win + 16 * h;
-        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
-        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
-        d[8] = v2.x; d[9] = v2.y; d[10] = v2.z; d[11] = v2.w;
-        d[12] = v3.x; d[13] = v3.y; d[14] = v3.z; d[15] = v3.w;
+    for (int h = 0; h < MT_WG / 8; h++) {            // 4 x (4 loads in flight, then 8 LDS stores)
+        const uint4 v0 = src[4 * h], v1 = src[4 * h + 1], v2 = src[4 * h + 2], v3 = src[4 * h + 3];
+        lds_u64 *d = win + 8 * h;
+        d[0] = (uint64_t)v0.x | ((uint64_t)v0.y << 32); d[1] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
+        d[2] = (uint64_t)v1.x | ((uint64_t)v1.y << 32); d[3] = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
+        d[4] = (uint64_t)v2.x | ((uint64_t)v2.y << 32); d[5] = (uint64_t)v2.z | ((uint64_t)v2.w << 32);
+        d[6] = (uint64_t)v3.x | ((uint64_t)v3.y << 32); d[7] = (uint64_t)v3.z | ((uint64_t)v3.w << 32);
     }
     return base;
 }
-
 template <int NW>
-__device__ __forceinline__ uint32_t win_word(Gen<NW> &G, uint64_t idx) {
-    uint64_t off = idx - G.wbase;
-    if (off >= MT_WIN) {
-        G.wbase = mt_refill(G.table, G.tlen, G.win, idx, G.err);
-        off = idx - G.wbase;
-        if (off >= MT_WIN) off = 0;   // only after MGX_DEVERR_MT_TABLE
+__device__ __forceinline__ uint64_t win_group(Gen<NW> &G, uint64_t g) {
+    uint64_t off = g - G.gbase;
+    if (off >= MT_WG) {
+        GCOUNT(G, 23);
+        G.gbase = mt_refill_cold(G.table, G.tlen, (lds_u64 *)G.win, g);
+        if (G.gbase == G.tlen) G.err |= 1u;
+        off = g - G.gbase;
+        if (off >= MT_WG) off = 0;   // only after MGX_DEVERR_MT_TABLE
     }
     return G.win[off];
 }
-// (re)load the register queue at the current cursor
+__device__ __forceinline__ uint64_t div10(uint64_t v) { return __umul64hi(v, 0xCCCCCCCCCCCCCCCDull) >> 3; }
+// (re)load the group registers at the current cursor
 template <int NW>
 __device__ __forceinline__ void mt_sync(Gen<NW> &G) {
-    G.q0 = win_word(G, G.cur);
-    G.q1 = win_word(G, G.cur + 1);
-    G.q2 = win_word(G, G.cur + 2);
-    G.q3 = win_word(G, G.cur + 3);
+    const uint64_t g = div10(G.cur);
+    G.go = (int)(G.cur - g * MT_FIELDS);
+    G.ga = win_group(G, g);
+    G.gb = win_group(G, g + 1);
+    G.gc = win_group(G, g + 2);
 }
-// getrandbits(32): the next MT19937 word of this env's stream (live-lock capped)
-template <int NW>
-__device__ __forceinline__ uint32_t mt_word(Gen<NW> &G) {
-    if (G.cur - G.astart >= G.llw) { G.abort = true; return 0; }
-    const uint32_t w = G.q0;
-    G.q0 = G.q1; G.q1 = G.q2; G.q2 = G.q3;
-    G.q3 = win_word(G, G.cur + 4);      // LDS read issued four draws before it is needed
-    G.cur++;
-    return w;
-}
-// random._randbelow_with_getrandbits(n), n >= 1
+// random._randbelow_with_getrandbits(n), 1 <= n < 32 (live-lock capped).
+// The reference draws getrandbits(k) = word >> (32 - k) until it is < n; on the 5-bit
+// field f of a word that is f < n << (5 - k).  Ten fields at once: guard-bit SWAR
+// subtract, first set guard = first accepted word.  One pass almost always suffices
+// (a lane needs another only after ten rejections), so lanes do not diverge here.
 template <int NW>
 __device__ __forceinline__ int randbelow(Gen<NW> &G, uint32_t n) {
+    GCOUNT(G, 24);
+    if (n >= 32u) { G.err |= 8u; return 0; }        // excluded by validation (n < 32 always)
     const int k = 32 - __clz(n);
+    const uint32_t sh = 5 - k;
+    const uint64_t c1 = (uint64_t)(32u + (n << sh) - 1u) * MT_REP;  // per slot: 32 + c - 1
     for (;;) {
-        const uint32_t w = mt_word(G);
-        if (G.abort) return 0;
-        const uint32_t r = k == 32 ? w : (w >> (32 - k));
-        if (r < n) return (int)r;
+        GCOUNT(G, 21);
+        const int o6 = 6 * G.go;
+        const uint64_t f = ((G.ga >> o6) | (o6 ? G.gb << (60 - o6) : 0ull)) & MT_LOW60;  // words cur..cur+9
+        const uint64_t acc = (c1 - f) & (32ull * MT_REP);   // guard bit of slot i <=> field i < c
+        const uint32_t left = G.llw - (uint32_t)(G.cur - G.astart);   // words this attempt may still take
+        const int j = acc ? (int)(((uint32_t)__ffsll((long long)acc) - 1u - 5u) * 171u >> 10) : MT_FIELDS;
+        int m = j < MT_FIELDS ? j + 1 : MT_FIELDS;         // words consumed by this pass
+        if ((uint32_t)m > left) {                           // cap reached before an accepted word
+            G.cur = G.astart + G.llw;
+            G.abort = true;
+            return 0;
+        }
+        const int r = (int)(((f >> (6 * (j < MT_FIELDS ? j : 0))) & 31u) >> sh);
+        G.cur += (uint64_t)m;
+        G.go += m;
+        if (G.go >= MT_FIELDS) {                            // next group: rotate, prefetch two ahead
+            G.go -= MT_FIELDS;
+            G.ga = G.gb;
+            G.gb = G.gc;
+            G.gc = win_group(G, div10(G.cur) + 2);
+        }
+        if (j < MT_FIELDS) return r;
     }
 }
 template <int NW>
@@ -362,6 +418,7 @@ template <int NW>
 __device__ __forceinline__ void add_obj(Gen<NW> &G, int t, int cname, int x, int y) {
     if (G.nobjs >= MAX_OBJS) { G.err |= 8u; return; }
     G.objs[G.nobjs++] = (uint32_t)t | ((uint32_t)(cname & 15) << 4) | ((uint32_t)x << 8) | ((uint32_t)y << 16);
+    G.tmask |= 1u << t;
 }
 
 // MiniGridEnv.place_obj position draw over the whole grid (PCG64): rejects occupied
@@ -369,6 +426,7 @@ __device__ __forceinline__ void add_obj(Gen<NW> &G, int t, int cname, int x, int
 template <int NW>
 __device__ __forceinline__ void draw_free_cell(Gen<NW> &G, int &px, int &py) {
     for (uint32_t it = 0;; ++it) {
+        GCOUNT(G, 22);
         if (it > PCG_LOOP_LIMIT) { G.err |= 4u; px = 1; py = 1; return; }
         const int x = pcg_integers(G.pcg, 0, G.S);
         const int y = pcg_integers(G.pcg, 0, G.S);
@@ -498,6 +556,40 @@ __device__ __forceinline__ void put_door(Gen<NW> &G, int x, int y, uint8_t code)
     if (y < S - 1) G.dn.set(b + S);
 }
 
+// Cells [x0, x1] x [y0, y1] that a placement loop would accept, as row masks of the
+// register bit sets (S <= 11): none -> the reference's `while True` never ends, so the
+// live-lock policy applies at once instead of after SAT_PROBE rejected draws (same
+// end state: the attempt's cursor jumps to its cap).  Excluded points: (-1,-1) = none.
+template <int NW>
+__device__ __forceinline__ uint32_t bits_row(const Bits<NW> &B, int y, int S) {
+    const int b = y * S;
+    uint64_t v = b < 64 ? (B.w0 >> b) : 0ull;
+    if (NW > 1) {
+        if (b >= 64) v = B.w1 >> (b - 64);
+        else if (b + S > 64) v |= B.w1 << (64 - b);
+    }
+    return (uint32_t)v & ((1u << S) - 1u);
+}
+template <int NW>
+__device__ __forceinline__ bool rect_has_free(const Gen<NW> &G, int x0, int x1, int y0, int y1, bool use_occ,
+                                              int ax, int ay, int bx, int by, int cx, int cy) {
+    if constexpr (NW == 4) {
+        return true;                      // S > 11: the in-loop SAT_PROBE check handles it
+    } else {
+        const uint32_t rowmask = ((1u << (x1 - x0 + 1)) - 1u) << x0;
+        bool sat = false;
+        for (int y = y0; y <= y1; y++) {
+            uint32_t bad = bits_row(G.dn, y, G.S);
+            if (use_occ) bad |= bits_row(G.occ, y, G.S);
+            if (ay == y && ax >= 0) bad |= 1u << ax;
+            if (by == y && bx >= 0) bad |= 1u << bx;
+            if (cy == y && cx >= 0) bad |= 1u << cx;
+            sat |= (rowmask & ~bad) != 0;
+        }
+        return sat;
+    }
+}
+
 // ---- multi-room layouts, table-driven (custom_env.py:617-2034) ---------------
 // One generic pass reproduces _generate_2/3/4_rooms: same RNG draws in the same
 // order, same Q1/Q5 quirks, one call site per primitive (keeps the generator
@@ -583,6 +675,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
         if (lk) { oc &= ~(1u << col); if (kib) oc &= ~(1u << (12 + col)); }
         dinfo |= (uint32_t)(col | (lk << 3) | (kib << 4)) << (8 * d);
     }
+    GSTAMP(G, 11);                                               // walls + door colour/lock draws
     if (G.abort) return;
     // door positions (custom_env.py:646-650, 911-930, 1365-1391)
 #pragma unroll 1
@@ -596,10 +689,12 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
         put_door(G, x, y, (uint8_t)door_code(di & 7, (di >> 3) & 1, open));
         add_obj(G, T_DOOR, di & 7, x, y);
     }
+    GSTAMP(G, 12);                                               // door positions
     if (G.abort) return;
     int gx, gy;
     place_goal_multi(G, gx, gy);
     place_agent(G);
+    GSTAMP(G, 13);                                               // goal + agent (PCG64)
     const int gr = room_of(nr, gx, gy, mid), ar = room_of(nr, G.ax, G.ay, mid);
     // object counters: c0 = (left | upper-left), c1 = (right | lower-left, unused by Q1), c2, c3
     const int n_left = G.num_objects / 2, n_right = G.num_objects - n_left;
@@ -607,36 +702,117 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     if (nr == 2) { c0 = n_left; c1 = n_right; c2 = c3 = 0; }
     else if (nr == 3) { c0 = n_left / 2; c1 = n_left - c0; c2 = n_right; c3 = 0; }
     else { c0 = n_left / 2; c1 = n_left - c0; c2 = n_right / 2; c3 = n_right - c2; }
-#pragma unroll 1
-    for (int r = 0; r < nr; r++) {
-        int x0, x1, y0, y1;
-        room_rect(nr, r, mid, S, x0, x1, y0, y1);
+    // Per room: which keys it gets (locked doors only) and how many objects (custom_env's
+    // decrement of the room counter by its keys and the goal; Q1: the lower-left room
+    // of the 3/4-room layouts loops over the upper-left counter).  No RNG involved.
+    uint32_t keymask = 0;   // room r: bit 2r = key A placed, bit 2r+1 = key B placed
+    uint32_t npack = 0;     // room r: byte r = objects to place (clamped at 0)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
         int kA, kB;
         bool chk;
         key_spec(nr, r, ar, kA, kB, chk);
-        int ndec = 0;
-        int kx = -1, ky = -1;
-        if (kA >= 0 && ((dinfo >> (8 * kA + 3)) & 1)) {
-            const uint32_t di = dinfo >> (8 * kA);
-            ndec++;
-            place_key(G, x0, x1, y0, y1, gx, gy, chk, -1, -1, di & 7, (di >> 4) & 1, &kx, &ky);
-            if (G.abort) return;
-        }
-        if (kB >= 0 && ((dinfo >> (8 * kB + 3)) & 1)) {
-            const uint32_t di = dinfo >> (8 * kB);
-            ndec++;
-            place_key(G, x0, x1, y0, y1, gx, gy, chk, kx, ky, di & 7, (di >> 4) & 1, (int *)nullptr, (int *)nullptr);
-            if (G.abort) return;
-        }
-        if (gr == r) ndec++;
+        const bool a = r < nr && kA >= 0 && ((dinfo >> (8 * kA + 3)) & 1);
+        const bool b = r < nr && kB >= 0 && ((dinfo >> (8 * kB + 3)) & 1);
+        keymask |= (uint32_t)a << (2 * r) | (uint32_t)b << (2 * r + 1);
+        const int ndec = (int)a + (int)b + (int)(gr == r);
         int n;
         if (r == 0) { c0 -= ndec; n = c0; }
-        else if (r == 1) { c1 -= ndec; n = (nr == 2) ? c1 : c0; }   // Q1: lower-left loops over c0
+        else if (r == 1) { c1 -= ndec; n = (nr == 2) ? c1 : c0; }
         else if (r == 2) { c2 -= ndec; n = c2; }
         else { c3 -= ndec; n = c3; }
-        place_objects(G, oc, MULTI_TYPES, n, x0, x1, y0, y1);
-        if (G.abort) return;
+        npack |= (uint32_t)(n > 0 ? n : 0) << (8 * r);
     }
+    // The keys and objects of all rooms as ONE task sequence executed by one flat loop:
+    // every iteration makes one placement attempt for every lane, whatever room/task the
+    // lane is at, so lanes no longer wait for each other at room and object boundaries
+    // (the nested room/key/object loops were the generator's dominant divergence).
+    // Each lane still draws exactly the reference's sequence:
+    //   for room r: [key A] [key B] then n_r x { choice(obj_choice); position loop }.
+    int r = 0, phase = 0, kleft = 0, kx = -1, ky = -1, rej = 0, ot = 0, ocn = 0;
+    bool chosen = false, fin = false;
+#pragma unroll 1
+    for (int it = 0; it < 12; it++) {            // advance to the first task (bounded)
+        if (phase == 0) { if ((keymask >> (2 * r)) & 1) break; phase = 1; }
+        if (phase == 1) { if ((keymask >> (2 * r + 1)) & 1) break; phase = 2; kleft = (npack >> (8 * r)) & 0xFF; }
+        if (kleft > 0) break;
+        if (++r >= nr) { fin = true; break; }
+        phase = 0;
+    }
+#pragma unroll 1
+    while (!fin) {
+        GCOUNT(G, 20);
+        int x0, x1, y0, y1;
+        room_rect(nr, r, mid, S, x0, x1, y0, y1);
+        const bool is_key = phase < 2;
+        int cname, ox = -1, oy = -1;
+        bool chk = false, kib = false;
+        if (is_key) {
+            int kA, kB;
+            key_spec(nr, r, ar, kA, kB, chk);
+            const uint32_t di = dinfo >> (8 * (phase == 0 ? kA : kB));
+            cname = di & 7;
+            kib = (di >> 4) & 1;
+            if (phase == 1) { ox = kx; oy = ky; }
+            if (rej == 0 && !rect_has_free(G, x0, x1, y0, y1, false, gx, gy, chk ? G.ax : -1, chk ? G.ay : -1, ox, oy)) {
+                live_lock(G); return;
+            }
+        } else {
+            if (!chosen) {
+                if (oc == 0) { G.err |= 8u; break; }
+                const int b = mask_choice(G, oc);
+                if (G.abort) return;
+                oc &= ~(1u << b);
+                ot = MULTI_TYPES[b / 6];
+                ocn = b % 6;
+                chosen = true;
+                if (!rect_has_free(G, x0, x1, y0, y1, true, G.ax, G.ay, -1, -1, -1, -1)) { live_lock(G); return; }
+            }
+            cname = ocn;
+        }
+        const int x = randint(G, x0, x1);
+        const int y = randint(G, y0, y1);
+        if (G.abort) return;
+        const bool bad = is_key ? ((x == gx && y == gy) || (chk && x == G.ax && y == G.ay) || (x == ox && y == oy) ||
+                                   next2door(G, x, y))
+                                : (occupied(G, y * S + x) || (x == G.ax && y == G.ay) || next2door(G, x, y));
+        if (bad) {
+            if (++rej == SAT_PROBE) {            // provably unsatisfiable loop -> live-lock policy
+                bool sat = false;
+                for (int xx = x0; xx <= x1 && !sat; xx++)
+                    for (int yy = y0; yy <= y1 && !sat; yy++)
+                        sat = is_key ? !((xx == gx && yy == gy) || (chk && xx == G.ax && yy == G.ay) ||
+                                         (xx == ox && yy == oy) || next2door(G, xx, yy))
+                                     : !(occupied(G, yy * S + xx) || (xx == G.ax && yy == G.ay) || next2door(G, xx, yy));
+                if (!sat) { live_lock(G); return; }
+            }
+            continue;
+        }
+        // commit the placement, then advance to the next task
+        const int cidx = cn2idx(cname);
+        if (is_key) {
+            if (kib) { put(G, x, y, mk_code(T_BOX, cidx, 1)); add_obj(G, T_BOX, cname, x, y); }
+            else { put(G, x, y, mk_code(T_KEY, cidx, 0)); add_obj(G, T_KEY, cname, x, y); }
+            if (phase == 0) { kx = x; ky = y; }
+            phase++;
+            if (phase == 2) kleft = (npack >> (8 * r)) & 0xFF;
+        } else {
+            put(G, x, y, mk_code(ot, cidx, 0));
+            add_obj(G, ot, cname, x, y);
+            chosen = false;
+            kleft--;
+        }
+        rej = 0;
+#pragma unroll 1
+        for (int k2 = 0; k2 < 12; k2++) {
+            if (phase == 1) { if ((keymask >> (2 * r + 1)) & 1) break; phase = 2; kleft = (npack >> (8 * r)) & 0xFF; }
+            if (phase == 2 && kleft > 0) break;
+            if (phase == 0) { if ((keymask >> (2 * r)) & 1) break; phase = 1; continue; }
+            if (++r >= nr) { fin = true; break; }
+            phase = 0; kx = -1; ky = -1;
+        }
+    }
+    GSTAMP(G, 14);                                               // keys + objects, room by room
 }
 
 template <int NW>
@@ -650,6 +826,7 @@ __device__ __forceinline__ int gen_multi(Gen<NW> &G) {             // custom_env
     if (G.abort) return 0;
     const int nr = randint(G, 2, 4);
     if (G.abort) return 0;
+    GSTAMP(G, 10);                                               // mission + room-count draws
     gen_rooms(G, nr);
     return cmd;
 }
@@ -719,7 +896,8 @@ __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
         G.occ.set(i * S); G.occ.set(i * S + S - 1);
     }
     G.dn.clear();
-    G.ax = -1; G.ay = -1; G.adir = 0; G.nobjs = 0;
+    G.ax = -1; G.ay = -1; G.adir = 0; G.nobjs = 0; G.tmask = 0;
+    GSTAMP(G, 9);                                                 // attempt setup (mt_sync, grid clear)
     const int cmd = G.problem == 0 ? gen_multi(G) : gen_single(G);
     if (G.abort) return;
     if (cmd == 0) {                                               // 'go to' (np_random.integers)
@@ -733,20 +911,13 @@ __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
         R.tx = (uint8_t)(o >> 8); R.ty = (uint8_t)(o >> 16); R.ta = A_DONE;
         R.mission_id = (uint8_t)(CMD_GOTO | (((o >> 4) & 15) << 2) | (type_slot(o & 15) << 5));
     } else if (cmd == 1 || cmd == 2) {                            // 'toggle' / 'pick up' (random.choice)
-        int i, rej = 0;
+        const uint32_t want = cmd == 1 ? (1u << T_BOX) | (1u << T_DOOR) : (1u << T_BOX) | (1u << T_KEY) | (1u << T_BALL);
+        if (!(G.tmask & want)) { live_lock(G); return; }     // no such object: the reference loops forever
+        int i;
         for (;;) {
             i = randbelow(G, (uint32_t)G.nobjs);
             if (G.abort) return;
-            const int t = G.objs[i] & 15;
-            if (cmd == 1 ? (t == T_BOX || t == T_DOOR) : (t == T_BOX || t == T_KEY || t == T_BALL)) break;
-            if (++rej == SAT_PROBE) {
-                bool sat = false;
-                for (int k = 0; k < G.nobjs; k++) {
-                    const int tk = G.objs[k] & 15;
-                    sat |= cmd == 1 ? (tk == T_BOX || tk == T_DOOR) : (tk == T_BOX || tk == T_KEY || tk == T_BALL);
-                }
-                if (!sat) { live_lock(G); return; }
-            }
+            if ((want >> (G.objs[i] & 15)) & 1) break;
         }
         const uint32_t o = G.objs[i];
         R.tx = (uint8_t)(o >> 8); R.ty = (uint8_t)(o >> 16);
@@ -767,10 +938,12 @@ template <int NW>
 __device__ __forceinline__ void reset_env(Gen<NW> &G, ResetOut &R) {
     R.livelocks = 0;
     for (;;) {
+        GSTAMP(G, 8);                   // previous episode's copy-out + loop
         G.astart = G.cur;
         G.abort = false;
         mt_sync(G);                     // register queue at the attempt's first word
         gen_attempt(G, R);
+        GSTAMP(G, 15);                  // mission target selection
         if (!G.abort) break;
         R.livelocks++;
         if (R.livelocks > 100000) { G.err |= 4u; break; }

@@ -32,6 +32,7 @@ using namespace mgx;
 namespace {
 
 constexpr int BLOCK_ENVS = 64;
+constexpr int MGX_NCOUNTERS = 32;          // [0..3] unused (per-workgroup slots), [4..7] step stamps, [8..] generator stamps
 constexpr int BLOCK_THREADS = 256;
 constexpr int FRAME = 147;                 // 3 x 7 x 7
 constexpr int FRAME_DW4 = 147;             // dwords per env row at n_stack == 4 (588 B)
@@ -43,11 +44,11 @@ struct KParams {
     uint8_t *grid;
     uint4 *pcg;        // [N][2]
     uint4 *aux;        // [N]
-    const uint32_t *mt;
+    const uint64_t *mt;             // packed MT19937(seed) stream: ten 5-bit fields per group
     const uint8_t *mtok;
     unsigned long long *counters;   // [0] steps [1] resets [2] livelocks [3] max cursor
     uint32_t *err;
-    uint64_t tlen;
+    uint64_t tlen;                  // groups
     int64_t n;
     int64_t seed_base;              // base_seed + env_index_offset
     int S, GS, GSL, grid_lds, n_stack, img_bytes, stk_lds, stk_step, problem, cfg_mission, num_objects, all_doors_open;
@@ -186,7 +187,7 @@ __device__ __forceinline__ void load_gen(Gen<NW> &G, const KParams &p, int64_t e
     G.table = p.mt;
     G.tlen = p.tlen;
     // lane >= 0: workgroup LDS layout [64 windows][64 objs lists]; lane < 0: one env's private block
-    G.win = reinterpret_cast<uint32_t *>(scratch + (lane >= 0 ? lane * (WIN_STRIDE * 4) : 0));
+    G.win = reinterpret_cast<uint64_t *>(scratch + (lane >= 0 ? lane * (WIN_STRIDE * 4) : 0));
     G.objs = reinterpret_cast<uint32_t *>(scratch + (lane >= 0 ? BLOCK_ENVS * (WIN_STRIDE * 4) + lane * (OBJ_STRIDE * 4)
                                                                : WIN_STRIDE * 4));
     G.llw = p.llw;
@@ -199,6 +200,10 @@ __device__ __forceinline__ void load_gen(Gen<NW> &G, const KParams &p, int64_t e
     G.nobjs = 0;
     G.ax = G.ay = -1;
     G.adir = 0;
+#ifdef MGX_GEN_STAMPS
+    G.stamps = p.counters;
+    G.tlast = __builtin_amdgcn_s_memtime();
+#endif
     gen_init(G);
 }
 
@@ -212,7 +217,7 @@ __device__ __forceinline__ void load_rng(Gen<NW> &G, const KParams &p, int64_t e
     G.pcg.uinteger = a.x;
     G.pcg.has = a.y;
     G.cur = (uint64_t)a.z | ((uint64_t)a.w << 32);
-    G.wbase = ~0ull >> 1;   // empty window
+    G.gbase = ~0ull >> 1;   // empty window
 }
 template <int NW>
 __device__ __forceinline__ void store_rng(const Gen<NW> &G, const KParams &p, int64_t e) {
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
             }
             G.cur = (uint64_t)c1.z | ((uint64_t)c1.w << 32);
         }
-        G.wbase = ~0ull >> 1;
+        G.gbase = ~0ull >> 1;
         ResetOut R;
         reset_env(G, R);
         st.ax = (uint8_t)G.ax; st.ay = (uint8_t)G.ay; st.dir = (uint8_t)G.adir; st.carry = 0;
@@ -861,9 +866,21 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
             Gen<NW> G;
             load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
             load_rng(G, p, e);
-            for (; nfree > 0; nfree--) {
+            int livelocks = 0;
+            // One attempt per iteration for every lane: a lane whose attempt live-locked
+            // retries while the others already generate their next episode (no wave-wide
+            // wait for the retry), exactly reset_env's retry semantics per env.
+            while (nfree > 0) {
                 ResetOut R;
-                reset_env(G, R);
+                G.astart = G.cur;
+                G.abort = false;
+                mt_sync(G);
+                gen_attempt(G, R);
+                if (G.abort && ++livelocks <= 100000) continue;
+                if (G.abort) G.err |= 4u;           // give up on this env (reported, never silent)
+                R.livelocks = livelocks;
+                livelocks = 0;
+                nfree--;
                 const int64_t slot = e * p.D + (tail & (p.D - 1));
                 uint4 *dst = reinterpret_cast<uint4 *>(p.ring_grid + slot * p.GS);
                 for (int c = 0; c < (p.GS >> 4); c++) {
@@ -1131,12 +1148,13 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->calls = 0;
     h->in_flight = false;
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 24;
-    h->cfg.mt_table_words = (h->cfg.mt_table_words + 3) & ~(int64_t)3;
+    h->cfg.mt_table_words = (h->cfg.mt_table_words + MT_FIELDS - 1) / MT_FIELDS * MT_FIELDS;
     const int64_t N = cfg->n_envs;
     const int S = cfg->size;
     const int GS = ((S * S) + 15) & ~15;
     const int IMG = FRAME * cfg->n_stack;
     const int64_t tlen = h->cfg.mt_table_words;
+    const int64_t ngroups = tlen / MT_FIELDS;         // whole groups only (a partial one is never read)
 
     auto bail = [&](mgx_status st) {
         for (void *&p : h->allocs) if (p) { (void)hipFree(p); p = nullptr; }
@@ -1145,7 +1163,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         return st;
     };
     size_t sizes[6] = {(size_t)N * sizeof(EnvState), (size_t)N * GS, (size_t)N * 32, (size_t)N * 16,
-                       (size_t)(tlen + MT_WIN + 4) * 4, 256 * 32 + 64};
+                       (size_t)(ngroups + MT_WG + 4) * 8, 256 * 32 + 64};
     for (int i = 0; i < 6; i++) {
         hipError_t e = hipMalloc(&h->allocs[i], sizes[i]);
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e)));
@@ -1165,18 +1183,22 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset fix list"));
     }
     {
-        hipError_t e = hipMalloc(&h->allocs[6], 8 * sizeof(unsigned long long) + 64);
+        hipError_t e = hipMalloc(&h->allocs[6], MGX_NCOUNTERS * sizeof(unsigned long long) + 64);
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc counters"));
-        e = hipMemset(h->allocs[6], 0, 8 * sizeof(unsigned long long) + 64);
+        e = hipMemset(h->allocs[6], 0, MGX_NCOUNTERS * sizeof(unsigned long long) + 64);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset counters"));
     }
-    // MT19937(base_seed) output table, zero-padded by one window
+    // MT19937(base_seed) output stream as packed top-5-bit fields (mgx_device.h: randbelow),
+    // zero-padded by one window
     {
-        std::vector<uint32_t> tab((size_t)(tlen + MT_WIN + 4), 0u);
+        std::vector<uint64_t> tab((size_t)(ngroups + MT_WG + 4), 0ull);
         HostMT m;
         m.seed((uint64_t)cfg->base_seed);
-        for (int64_t i = 0; i < tlen; i++) tab[(size_t)i] = m.next();
-        hipError_t e = hipMemcpy(h->allocs[4], tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
+        for (int64_t i = 0; i < tlen; i++) {
+            const uint64_t f = m.next() >> 27;
+            tab[(size_t)(i / MT_FIELDS)] |= f << (6 * (i % MT_FIELDS));
+        }
+        hipError_t e = hipMemcpy(h->allocs[4], tab.data(), tab.size() * 8, hipMemcpyHostToDevice);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "upload MT table"));
     }
     {
@@ -1193,11 +1215,11 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.grid = (uint8_t *)h->allocs[1];
     p.pcg = (uint4 *)h->allocs[2];
     p.aux = (uint4 *)h->allocs[3];
-    p.mt = (const uint32_t *)h->allocs[4];
+    p.mt = (const uint64_t *)h->allocs[4];
     p.mtok = (const uint8_t *)h->allocs[5];
     p.counters = (unsigned long long *)h->allocs[6];
-    p.err = (uint32_t *)((char *)h->allocs[6] + 8 * sizeof(unsigned long long));
-    p.tlen = (uint64_t)tlen;
+    p.err = (uint32_t *)((char *)h->allocs[6] + MGX_NCOUNTERS * sizeof(unsigned long long));
+    p.tlen = (uint64_t)ngroups;
     p.n = N;
     p.seed_base = cfg->base_seed + cfg->env_index_offset;
     p.S = S;
@@ -1357,6 +1379,14 @@ mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, v
     HIP_TRY(hipGetLastError());
     h->calls = 0;
     return launch_refill(h, stream);            // fills every ring (synchronously on `stream`)
+}
+
+mgx_status mgx_debug_counters(mgx_handle *h, void *stream, uint64_t *out, int n) {
+    if (!h || !out || n < 0 || n > MGX_NCOUNTERS) return fail(MGX_ERR_INVALID, "bad argument");
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize(h->side));
+    HIP_TRY(hipMemcpy(out, h->kp.counters, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return MGX_OK;
 }
 
 mgx_status mgx_set_seed(mgx_handle *h, int64_t seed) {

@@ -22,7 +22,7 @@ DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unk
 
 # Every entry point include/mgx.h declares (checked by tests/test_abi.py).
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
-           "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_poll_error", "mgx_stats", "mgx_dump_state", "mgx_mission_text")
+           "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text")
 
 
 class MgxConfig(ctypes.Structure):
@@ -80,6 +80,7 @@ def load():
     L.mgx_gae.argtypes = [P, P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P]
     L.mgx_poll_error.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]
     L.mgx_stats.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64)]
+    L.mgx_debug_counters.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.mgx_dump_state.argtypes = [P, P] + [P] * 10
     L.mgx_mission_text.argtypes = [I, ctypes.c_char_p, ctypes.c_size_t]
     for name in EXPORTS:

@@ -149,6 +149,12 @@ class MgxEngine:
         return dict(steps=int(out[0]), resets=int(out[1]), livelocks=int(out[2]), max_mt_cursor=int(out[3]),
                     phase_clocks=[int(out[i]) for i in range(4, 8)])
 
+    def debug_counters(self, n=32):
+        """Raw diagnostic counters (section clocks of the stamp builds)."""
+        out = (ctypes.c_uint64 * n)()
+        _lib.check(self.L.mgx_debug_counters(self.h, self._stream(), out, n), "mgx_debug_counters")
+        return [int(v) for v in out]
+
     def dump_state(self):
         import numpy as np
         n, S = self.n, self.size
