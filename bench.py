@@ -97,6 +97,16 @@ def _cpu_model():
     return "unknown"
 
 
+def _allreduce(t, op):
+    """all_reduce on the backend's device (RCCL: GPU tensors; gloo rehearsal: CPU)."""
+    if dist.get_backend() == "gloo":
+        c = t.cpu()
+        dist.all_reduce(c, op=op)
+        return c.to(t.device)
+    dist.all_reduce(t, op=op)
+    return t
+
+
 def main_ppo(args, world, rank, local, dev):
     """BASELINE config 3: PPO(CustomPPOPolicy) on PKP 8x8 with the engine (mgx/ppo.py)."""
     from mgx.policy import ActorCriticPolicy
@@ -149,7 +159,7 @@ def main_ppo(args, world, rank, local, dev):
         dist.barrier()
     wall = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+        wall = _allreduce(wall, dist.ReduceOp.MAX)
     eng.poll_error()
     wall = float(wall[0])
     if rank == 0:
@@ -176,11 +186,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; `local % device_count` only matters for a rehearsal of the
+    # N>1 path with more ranks than GPUs (MGX_DIST_BACKEND=gloo: RCCL refuses shared GPUs)
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)
+    backend = os.environ.get("MGX_DIST_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if args.workload == "ppo":
         return main_ppo(args, world, rank, local, dev)
     from mgx import MgxEngine
@@ -253,8 +271,8 @@ def main():
     steps_done = torch.tensor([float(st1["steps"] - st0["steps"]), float(st1["resets"] - st0["resets"])],
                               dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(steps_done, op=dist.ReduceOp.SUM)
+        elapsed = _allreduce(elapsed, dist.ReduceOp.MAX)
+        steps_done = _allreduce(steps_done, dist.ReduceOp.SUM)
     wall_max, gpu_max = float(elapsed[0]), float(elapsed[1])
     total_env_steps, total_resets = float(steps_done[0]), float(steps_done[1])
     assert int(total_env_steps) == n * K * world, (total_env_steps, n * K * world)
