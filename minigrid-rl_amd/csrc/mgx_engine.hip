@@ -109,6 +109,18 @@ __device__ __forceinline__ void grid_copy_out(uint8_t *g, const uint8_t *lds, in
     }
 }
 
+// Image-stack stores (diagnostic switch: -DMGX_NT_STACK = non-temporal)
+__device__ __forceinline__ void stk_store(uint4 *p, uint4 v) {
+#ifdef MGX_NT_STACK
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+    __builtin_nontemporal_store(v.z, &p->z);
+    __builtin_nontemporal_store(v.w, &p->w);
+#else
+    *p = v;
+#endif
+}
+
 // Mission-stack slot writer: slot `s` of env row gets mission tokens or zeros.
 __device__ __forceinline__ void write_mission_slot(void *mis, int mission64, int64_t e, int n_stack, int s,
                                                    const uint8_t *tok /* null = zeros */) {
@@ -384,6 +396,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     const int FSTRIDE = fast ? FROW : IMG, FOFF = fast ? 1 : 0;
     __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params ax | ay<<8 | dir<<16 | carry<<24
     __shared__ uint8_t s_done[BLOCK_ENVS];
+    __shared__ uint8_t s_term[BLOCK_ENVS];       // done env whose stacked terminal_observation is written
     __shared__ uint8_t s_dirty[BLOCK_ENVS];
     __shared__ uint8_t s_dlist[BLOCK_ENVS];      // envs that popped a new episode (render + mission lists)
     __shared__ uint8_t s_flist[BLOCK_ENVS];      // envs whose mission stack is still filling
@@ -438,6 +451,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
             }
         }
     }
+    // ... and for the tail dword of a partial block (not a multiple of 4 dwords)
+    const int kt = nq * 4 + tid;
+    uint32_t tq36 = 0, tq37 = 0;
+    if (fast && kt < limit) {
+        tq36 = g32in[kt + 36];
+        if (kt + 37 < limit) tq37 = g32in[kt + 37];
+    }
     // (c) grids -> LDS (and, staged path, the whole old stacks -> LDS)
     {
         const int q = p.GS >> 4;
@@ -471,6 +491,40 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
 #ifdef MGX_STAMPS
     ts1 = __builtin_amdgcn_s_memtime();
 #endif
+    // ---- phase 1b (fast roll, pass 1): store the shifted OLD part of every row now
+    // (output dword j <= 109 of a row = old dwords j+36, j+37 aligned by 3 bytes), as if
+    // no env were done.  The old dwords are in registers (loaded before the barrier
+    // above), so these stores drain while wave 0 runs the step logic and the block
+    // renders.  Pass 2 (phase 3) writes what depends on this step: the new frame
+    // (j >= 110) and the zeroed old part of done envs.
+    if (fast) {
+        uint32_t *g32 = reinterpret_cast<uint32_t *>(o.img + e0 * (int64_t)IMG);
+        uint4 *g128 = reinterpret_cast<uint4 *>(g32);
+#pragma unroll
+        for (int r = 0; r < MAXQ; r++) {
+            const int q = r * BLOCK_THREADS + tid, k = 4 * q;
+            if (q < nq) {
+                const uint32_t src[5] = {qa[r].x, qa[r].y, qa[r].z, qa[r].w, qb[r]};
+                int j = k - (k / DW) * DW;
+                uint32_t w[4];
+                bool ok[4];
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    ok[t] = j <= 109;
+                    w[t] = __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
+                    if (++j == DW) j = 0;
+                }
+                if (ok[0] && ok[1] && ok[2] && ok[3]) {
+                    stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4; t++)
+                        if (ok[t]) g32[k + t] = w[t];
+                }
+            }
+        }
+        // tail dword of a partial block: written in pass 2 only
+    }
 
     // ---- phase 2a: one lane per env: MiniGridEnv.step + PlaygroundEnv.step
     uint32_t my_err = 0;
@@ -580,8 +634,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
             if (o.livelock) o.livelock[e] = 0;
         }
         s_done[tid] = done;
+        s_term[tid] = done && (p.terminal_mode == MGX_TERMINAL_ALL ||
+                               (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term));
     } else if (tid < BLOCK_ENVS) {
         s_done[tid] = 0;
+        s_term[tid] = 0;
     }
     if (tid < BLOCK_ENVS) {                            // wave 0: ballot compaction of the fill list
         const unsigned long long fm = __ballot(fill), dm = __ballot(done);
@@ -610,8 +667,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
             if (p.terminal_mode == MGX_TERMINAL_ALL || (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term)) {
                 // re-stacked like VecFrameStack (rare -> per-lane writes): older frames, then the terminal one
                 uint8_t *t = o.t_img + e * (int64_t)IMG;
-                const uint8_t *old = fast ? o.img + e * (int64_t)IMG : s_stk + tid * IMG;
-                for (int off = 0; off < IMG - FRAME; off++) t[off] = old[off + FRAME];
+                if (!fast) {             // fast path: the quad owners write the older frames in phase 3
+                    const uint8_t *old = s_stk + tid * IMG;
+                    for (int off = 0; off < IMG - FRAME; off++) t[off] = old[off + FRAME];
+                }
                 for (int k = 0; k < FRAME; k++) t[IMG - FRAME + k] = fr[k];
                 if (p.n_stack == 4)
                     reinterpret_cast<uint4 *>(o.t_dir)[e] = make_uint4(odir.y, odir.z, odir.w, 1u << (8 * dir));
@@ -716,30 +775,42 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                 const uint32_t src[5] = {qa[r].x, qa[r].y, qa[r].z, qa[r].w, qb[r]};
                 int e = k / DW, j = k - e * DW;
                 uint32_t w[4];
+                bool need = false;                   // pass 1 already stored this quad as-is?
 #pragma unroll
                 for (int t = 0; t < 4; t++) {
                     const bool dn = s_done[e];
+                    need |= dn || j >= 110;
                     uint32_t out;
                     if (j <= 109) out = dn ? 0u : __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
                     else if (j == 110) out = (f32[e * (FROW / 4)] & 0xFFFFFF00u) | (dn ? 0u : (src[t] >> 24));
                     else out = f32[e * (FROW / 4) + (j - 110)];
                     w[t] = out;
+                    if (s_term[e]) {                 // terminal_observation: the older frames (rare)
+                        uint8_t *trow = o.t_img + (e0 + e) * (int64_t)IMG;
+                        if (j <= 109) reinterpret_cast<uint32_t *>(trow)[j] = __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
+                        else if (j == 110) trow[4 * 110] = (uint8_t)(src[t] >> 24);   // old byte 587
+                    }
                     if (++j == DW) { j = 0; e++; }
                 }
-                g128[q] = make_uint4(w[0], w[1], w[2], w[3]);
+                if (need) stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
             }
         }
         // tail dword (partial last block whose row count is not a multiple of 4): its old
         // dwords come from rows no other thread of this block writes before the barrier below
         if (limit != nq * 4) {
-            const int kt = nq * 4 + tid;
             uint32_t tv = 0;
             if (kt < limit) {
                 const int e = kt / DW, j = kt - e * DW;
                 const bool dn = s_done[e];
-                if (j <= 109) tv = dn ? 0u : __builtin_amdgcn_alignbyte(g32in[kt + 37], g32in[kt + 36], 3);
-                else if (j == 110) tv = (f32[e * (FROW / 4)] & 0xFFFFFF00u) | (dn ? 0u : (g32in[kt + 36] >> 24));
+                const uint32_t o36 = tq36, o37 = tq37;
+                if (j <= 109) tv = dn ? 0u : __builtin_amdgcn_alignbyte(o37, o36, 3);
+                else if (j == 110) tv = (f32[e * (FROW / 4)] & 0xFFFFFF00u) | (dn ? 0u : (o36 >> 24));
                 else tv = f32[e * (FROW / 4) + (j - 110)];
+                if (s_term[e]) {
+                    uint8_t *trow = o.t_img + (e0 + e) * (int64_t)IMG;
+                    if (j <= 109) reinterpret_cast<uint32_t *>(trow)[j] = __builtin_amdgcn_alignbyte(o37, o36, 3);
+                    else if (j == 110) trow[4 * 110] = (uint8_t)(o36 >> 24);
+                }
             }
             __syncthreads();
             if (kt < limit) reinterpret_cast<uint32_t *>(o.img + e0 * (int64_t)IMG)[kt] = tv;

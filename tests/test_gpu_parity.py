@@ -253,3 +253,46 @@ def test_sharded_engines_equal_one_engine():
     sp = [p.stats() for p in parts]
     assert sw["resets"] == sum(s["resets"] for s in sp)
     whole.poll_error()
+
+
+@pytest.mark.parametrize("n,terminal_mode", [(77, "all"), (130, "truncated")])
+def test_ragged_block_full_stacks_match_oracle(n, terminal_mode):
+    """A partial last workgroup (n not a multiple of 64, rows not a multiple of 4
+    dwords): full stacked observation and stacked terminal_observation every step,
+    against the C oracle + the numpy VecFrameStack restatement."""
+    _need_gpu()
+    import oracle as O
+    from mgx import MgxEngine
+    T = 160
+    ov = O.OracleVec("multi", None, 8, 4, n, 42)
+    fs = O.FrameStackOracle(n, 4)
+    eng = MgxEngine(problem="multi", mission=None, size=8, n_envs=n, n_stack=4, terminal_mode=terminal_mode)
+
+    def raw(img, dr, mi):
+        return dict(image=O.vec_transpose_image(img), direction=O.one_hot_dir(dr), mission=mi.astype(np.int64))
+
+    r = ov.reset()
+    want = fs.reset(raw(r["image"], r["dir"], r["mission"]))
+    obs = eng.reset()
+    for k in want:
+        assert np.array_equal(obs[k].to(torch.int64).cpu().numpy(), want[k].astype(np.int64)), k
+    rng = np.random.default_rng(7)
+    n_term = 0
+    for t in range(T):
+        a = rng.integers(0, 7 if terminal_mode == "all" else 6, n)   # no 'done' -> truncations
+        o = ov.step(a.astype(np.int32))
+        done = (o["terminated"] | o["truncated"]).astype(bool)
+        cur = raw(np.where(done[:, None, None, None], o["r_image"], o["image"]), np.where(done, o["r_dir"], o["dir"]),
+                  np.where(done[:, None], o["r_mission"], o["mission"]))
+        want, want_term = fs.step(cur, done, raw(o["image"], o["dir"], o["mission"]))
+        obs = eng.step(torch.as_tensor(a, device=eng.device))
+        for k in want:
+            assert np.array_equal(obs[k].to(torch.int64).cpu().numpy(), want[k].astype(np.int64)), (t, k)
+        sel = done if terminal_mode == "all" else (o["truncated"].astype(bool) & ~o["terminated"].astype(bool))
+        if sel.any():
+            n_term += int(sel.sum())
+            for k in want_term:
+                got = eng.terminal_obs[k].to(torch.int64).cpu().numpy()[sel]
+                assert np.array_equal(got, want_term[k][sel].astype(np.int64)), (t, k)
+    assert n_term > 0
+    eng.poll_error()
