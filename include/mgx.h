@@ -81,12 +81,13 @@ typedef struct mgx_config {
     int32_t livelock_words;    /* 0 -> MGX_LIVELOCK_WORDS */
     int32_t terminal_mode;     /* mgx_terminal_mode */
     int32_t mission_int64;     /* 1: mission tokens int64 (TokenizeVocabWrapper dtype), 0: uint8 */
-    int32_t reserved;
+    int32_t refill_cap;        /* episodes an env may pre-generate per refill epoch beyond what keeps the
+                                  ring from running dry (0 -> 6, < 0 -> fill the ring) */
     int64_t mt_table_words;    /* 0 -> default (2^24); shared MT19937 output table length */
-    int32_t ring_depth;        /* pre-generated episodes per env (0 -> 64; rounded up to a power of two
+    int32_t ring_depth;        /* pre-generated episodes per env (0 -> 128; rounded up to a power of two
                                   <= 128; -1 = no ring: every auto-reset generated inline) */
-    int32_t refill_every;      /* steps per refill epoch K (0 -> ring_depth/2; clamped to <= ring_depth/2,
-                                  which guarantees the ring never runs dry: a step pops <= 1 episode) */
+    int32_t refill_every;      /* steps per refill epoch K (0 -> ring_depth/4; clamped to <= ring_depth/2:
+                                  each epoch keeps >= K queued, and a step pops <= 1 episode) */
 } mgx_config;
 
 /* Stacked observation in the layout SB3's VecFrameStack(VecTransposeImage(.))

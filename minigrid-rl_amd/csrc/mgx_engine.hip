@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -69,6 +70,9 @@ struct KParams {
     ulonglong4 *blk;        // [3 * nblk] per-workgroup stats: step/reset | fixup | refill workgroups
     int nblk;               // ceil(N / 64)
     int D;
+    int K;                  // refill epoch (steps)
+    int cap;                // episodes an env produces per epoch beyond what the invariant needs (<0: fill to D)
+    int initial_fill;       // this refill launch is mgx_reset's (fill every ring to 2K)
     int reset_mode;         // mgx_reset: 0 first (seeded, MT cursor 0), 1 seeded, 2 unseeded
 };
 
@@ -932,7 +936,14 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
         // (older, smaller), which only under-estimates the free slots.
         const uint8_t head = *reinterpret_cast<volatile const uint8_t *>(p.ring_head + e);
         uint8_t tail = p.ring_tail[e];
-        int nfree = p.D - (int)(uint8_t)(tail - head);
+        // Production: at least what keeps >= K episodes queued at the next join (each step
+        // pops <= 1, so 2K - level), plus up to `cap` more while there is room.  Capping the
+        // per-epoch production balances work across the lanes of a wave (its time is the
+        // busiest lane's) while rings with slack absorb bursts of short episodes.
+        const int level = (int)(uint8_t)(tail - head);
+        const int space = p.D - level, need = 2 * p.K - level;
+        int nfree = p.initial_fill ? need : max(need, p.cap < 0 ? space : min(p.cap, space));
+        nfree = min(nfree, space);
         if (nfree > 0) {
             Gen<NW> G;
             load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
@@ -1142,6 +1153,7 @@ struct mgx_handle {
     uint64_t resets;        // mgx_reset calls since create
     bool seed_pending;      // mgx_set_seed called since the last reset
     bool in_flight;         // a refill forked and not yet joined
+    bool serial_refill;     // diagnostics (env MGX_SERIAL_REFILL=1): refill on the caller's stream
     hipStream_t side;       // refill stream
     hipEvent_t ev_fork, ev_done;
     void *allocs[16];
@@ -1205,7 +1217,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->cfg = *cfg;
     h->device = device;
     if (h->cfg.livelock_words <= 0) h->cfg.livelock_words = MGX_LIVELOCK_WORDS;
-    if (h->cfg.ring_depth == 0) h->cfg.ring_depth = 64;
+    if (h->cfg.ring_depth == 0) h->cfg.ring_depth = 128;
     if (h->cfg.ring_depth < 0) {
         h->cfg.ring_depth = 0;                                   // ring disabled: every reset generated inline
     } else {
@@ -1213,11 +1225,16 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         while (d < h->cfg.ring_depth && d < 128) d <<= 1;        // power of two (mod-256 ring indices)
         h->cfg.ring_depth = d;
     }
-    if (h->cfg.refill_every <= 0 || h->cfg.refill_every > h->cfg.ring_depth / 2)
-        h->cfg.refill_every = std::max(1, h->cfg.ring_depth / 2);
+    if (h->cfg.refill_every <= 0) h->cfg.refill_every = std::max(1, h->cfg.ring_depth / 4);
+    if (h->cfg.refill_every > h->cfg.ring_depth / 2) h->cfg.refill_every = std::max(1, h->cfg.ring_depth / 2);
+    if (h->cfg.refill_cap == 0) h->cfg.refill_cap = 6;
     h->refill_every = h->cfg.refill_every;
     h->calls = 0;
     h->in_flight = false;
+    {
+        const char *sv = std::getenv("MGX_SERIAL_REFILL");
+        h->serial_refill = sv && sv[0] == '1';
+    }
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 24;
     h->cfg.mt_table_words = (h->cfg.mt_table_words + MT_FIELDS - 1) / MT_FIELDS * MT_FIELDS;
     const int64_t N = cfg->n_envs;
@@ -1328,6 +1345,9 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         p.blk = (ulonglong4 *)h->allocs[13];
     }
     p.D = D;
+    p.K = h->cfg.refill_every;
+    p.cap = h->cfg.refill_cap;
+    p.initial_fill = 0;
     p.mission64 = cfg->mission_int64;
     h->lds_step = (size_t)p.stk_step + (size_t)p.grid_lds;
     h->lds_reset = (size_t)p.stk_lds + (size_t)p.grid_lds;
@@ -1397,6 +1417,7 @@ static mgx_status join_refill(mgx_handle *h, void *stream) {
 static mgx_status fork_refill(mgx_handle *h, void *stream) {
     HIP_TRY(hipMemcpyAsync(h->kp.ring_pub, h->kp.ring_tail, (size_t)h->kp.n, hipMemcpyDeviceToDevice,
                            (hipStream_t)stream));
+    if (h->serial_refill) return launch_refill(h, stream);
     HIP_TRY(hipEventRecord(h->ev_fork, (hipStream_t)stream));
     HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
     mgx_status s = launch_refill(h, h->side);
@@ -1449,7 +1470,10 @@ mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, v
     }
     HIP_TRY(hipGetLastError());
     h->calls = 0;
-    return launch_refill(h, stream);            // fills every ring (synchronously on `stream`)
+    h->kp.initial_fill = 1;                     // fills every ring to 2K (synchronously on `stream`)
+    const mgx_status rs = launch_refill(h, stream);
+    h->kp.initial_fill = 0;
+    return rs;
 }
 
 mgx_status mgx_debug_counters(mgx_handle *h, void *stream, uint64_t *out, int n) {

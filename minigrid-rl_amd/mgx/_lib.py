@@ -32,7 +32,7 @@ class MgxConfig(ctypes.Structure):
         ("all_doors_open", ctypes.c_int32), ("obstacles", ctypes.c_int32), ("n_stack", ctypes.c_int32),
         ("n_envs", ctypes.c_int64), ("base_seed", ctypes.c_int64), ("env_index_offset", ctypes.c_int64),
         ("livelock_words", ctypes.c_int32), ("terminal_mode", ctypes.c_int32),
-        ("mission_int64", ctypes.c_int32), ("reserved", ctypes.c_int32), ("mt_table_words", ctypes.c_int64),
+        ("mission_int64", ctypes.c_int32), ("refill_cap", ctypes.c_int32), ("mt_table_words", ctypes.c_int64),
         ("ring_depth", ctypes.c_int32), ("refill_every", ctypes.c_int32),
     ]
 

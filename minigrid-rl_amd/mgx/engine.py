@@ -25,7 +25,7 @@ class MgxEngine:
                  env_index_offset=0, n_stack=4, all_doors_open=False, see_through_walls=True,
                  obstacles=False, terminal_mode="truncated", mission_dtype=torch.int64,
                  device="cuda", livelock_words=0, mt_table_words=0, reward64=False, ring_depth=0,
-                 refill_every=0):
+                 refill_every=0, refill_cap=0):
         self.L = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.MgxError("MgxEngine needs a GPU (no CPU fallback by design)")
@@ -57,6 +57,7 @@ class MgxEngine:
         cfg.mt_table_words = int(mt_table_words)
         cfg.ring_depth = int(ring_depth)
         cfg.refill_every = int(refill_every)
+        cfg.refill_cap = int(refill_cap)
         self.terminal_mode = terminal_mode
         self.mission_dtype = torch.int64 if cfg.mission_int64 else torch.uint8
         h = _P()

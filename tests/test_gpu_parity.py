@@ -296,3 +296,31 @@ def test_ragged_block_full_stacks_match_oracle(n, terminal_mode):
                 assert np.array_equal(got, want_term[k][sel].astype(np.int64)), (t, k)
     assert n_term > 0
     eng.poll_error()
+
+
+@pytest.mark.parametrize("ring", [(0, 0, 0), (16, 4, 1), (8, 4, -1)], ids=["default", "d16_k4_cap1", "d8_k4_fill"])
+def test_ring_never_runs_dry_under_max_consumption(ring):
+    """Every env resets every step ('done' action: one episode per step, the most a
+    step can consume) -- the refill's production rule must keep every ring non-empty
+    (no MGX_DEVERR_RING_EMPTY) and the stream must stay bit-exact with the oracle."""
+    _need_gpu()
+    import oracle as O
+    from mgx import MgxEngine
+    n, T = 512, 160
+    ov = O.OracleVec("multi", None, 8, 4, n, 42)
+    eng = MgxEngine(problem="multi", mission=None, size=8, n_envs=n, terminal_mode="none",
+                    ring_depth=ring[0], refill_every=ring[1], refill_cap=ring[2])
+    ov.reset()
+    eng.reset()
+    rng = np.random.default_rng(3)
+    for t in range(T):
+        a = np.full(n, 6) if t % 40 < 30 else rng.integers(0, 7, n)   # bursts of 'done', then random
+        o = ov.step(a.astype(np.int32))
+        obs = eng.step(torch.as_tensor(a, device=eng.device))
+        img, dr, mi = EngineSource.newest(obs)
+        done = (o["terminated"] | o["truncated"]).astype(bool)
+        assert np.array_equal(img, np.where(done[:, None, None, None], o["r_image"], o["image"])), t
+    eng.poll_error()            # raises on MGX_DEVERR_RING_EMPTY
+    a_, b_ = eng.dump_state(), ov.dump()
+    for k in ("grid", "agent", "mtwords", "pcg"):
+        assert np.array_equal(a_[k], b_[k]), k
