@@ -32,6 +32,9 @@ using namespace mgx;
 
 namespace {
 
+#ifndef MGX_DIAG_SKIP
+#define MGX_DIAG_SKIP 0     // diagnostics only: skip store classes (1 pass-1, 2 pass-2, 4 missions, 16 grids)
+#endif
 constexpr int BLOCK_ENVS = 64;
 constexpr int MGX_NCOUNTERS = 32;          // [0..3] unused (per-workgroup slots), [4..7] step stamps, [8..] generator stamps
 constexpr int BLOCK_THREADS = 256;
@@ -443,7 +446,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
             const int q = r * BLOCK_THREADS + tid, k = 4 * q;
             qa[r] = make_uint4(0, 0, 0, 0);
             qb[r] = 0;
-            if (q < nq) {
+            // quads wholly inside a row's new-frame columns (111..146) need no old data:
+            // skipping them saves the dropped oldest frame's 147 B per env of reads
+            const int j0 = k - (k / DW) * DW;
+            if (q < nq && !(j0 >= 111 && j0 <= DW - 4)) {
                 if (k + 39 < limit) {
                     qa[r] = *reinterpret_cast<const uint4 *>(g32in + k + 36);          // 16-B aligned
                 } else {                                                               // last row: stay inside
@@ -519,11 +525,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                     if (++j == DW) j = 0;
                 }
                 if (ok[0] && ok[1] && ok[2] && ok[3]) {
-                    stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
+                    if (!(MGX_DIAG_SKIP & 1)) stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
                 } else {
 #pragma unroll
                     for (int t = 0; t < 4; t++)
-                        if (ok[t]) g32[k + t] = w[t];
+                        if (!(MGX_DIAG_SKIP & 1)) if (ok[t]) g32[k + t] = w[t];
                 }
             }
         }
@@ -746,13 +752,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         for (int w = tid; w < tot_d; w += BLOCK_THREADS) {
             const int i = w / per, j = w - i * per;
             const int le = s_dlist[i], sl = j / CPS, c = j - sl * CPS;
-            write_mission_chunk(o.mis, p.mission64, e0 + le, K, sl, c, sl == K - 1 ? p.mtok + s_mid[le] * 32 : nullptr);
+            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk(o.mis, p.mission64, e0 + le, K, sl, c, sl == K - 1 ? p.mtok + s_mid[le] * 32 : nullptr);
         }
         const int tot_f = s_nf * CPS;
         for (int w = tid; w < tot_f; w += BLOCK_THREADS) {
             const int i = w / CPS, c = w - i * CPS;
             const int le = s_flist[i];
-            write_mission_chunk(o.mis, p.mission64, e0 + le, K, s_fslot[le], c, p.mtok + s_mid[le] * 32);
+            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk(o.mis, p.mission64, e0 + le, K, s_fslot[le], c, p.mtok + s_mid[le] * 32);
         }
     }
     if (tid < BLOCK_ENVS) s_dirty[tid] = dirty;
@@ -796,7 +802,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                     }
                     if (++j == DW) { j = 0; e++; }
                 }
-                if (need) stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
+                if (!(MGX_DIAG_SKIP & 2)) if (need) stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
             }
         }
         // tail dword (partial last block whose row count is not a multiple of 4): its old
@@ -832,7 +838,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     }
 
     // ---- phase 5: write back grids that changed (moves, pickups, resets)
-    grid_copy_out(p.grid + e0 * p.GS, s_grid, ne, p.GS, p.GSL, s_dirty);
+    if (!(MGX_DIAG_SKIP & 16)) grid_copy_out(p.grid + e0 * p.GS, s_grid, ne, p.GS, p.GSL, s_dirty);
     if (tid == 0) {
         // workgroup-private stats slot: fire-and-forget adds (no load on the kernel's tail)
         atomicAdd(&p.blk[blockIdx.x].x, (unsigned long long)ne);
