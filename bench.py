@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--probe", type=int, default=256, help="eager steps timed per launch for the roofline")
     ap.add_argument("--workload", default="rollout", choices=["rollout", "ppo"])
     ap.add_argument("--horizon", type=int, default=16, help="ppo: env steps per rollout")
-    ap.add_argument("--batch-size", type=int, default=16384, help="ppo: minibatch size")
+    ap.add_argument("--batch-size", type=int, default=65536, help="ppo: minibatch size")
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
     return ap.parse_args()
 

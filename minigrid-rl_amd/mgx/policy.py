@@ -38,6 +38,27 @@ DEFAULT_ARCH = {
 OBS_KEYS = ("direction", "image", "mission")          # observation-space (Dict) key order
 
 
+class Conv2dGemm(nn.Conv2d):
+    """nn.Conv2d (same parameters, init and state_dict) computed as ONE GEMM over the
+    whole batch: the kh*kw shifted views are concatenated along channels (im2col
+    without a per-sample loop; ATen's unfold and MIOpen's GEMM algorithms launch per
+    sample at batch 16k+) and contracted with the weight in a single matmul.
+    Stride 1, no padding/dilation/groups (the reference's convs); else nn.Conv2d."""
+
+    def forward(self, x):
+        if (self.padding_mode != "zeros" or self.groups != 1 or tuple(self.stride) != (1, 1)
+                or tuple(self.dilation) != (1, 1) or any(self.padding)):
+            return super().forward(x)
+        B, C, H, W = x.shape
+        kh, kw = self.kernel_size
+        oh, ow = H - kh + 1, W - kw + 1
+        cols = torch.cat([x[:, :, dy:dy + oh, dx:dx + ow] for dy in range(kh) for dx in range(kw)], dim=1)
+        cols = cols.permute(0, 2, 3, 1).reshape(B * oh * ow, kh * kw * C)           # [(b,y,x), (dy,dx,c)]
+        wt = self.weight.permute(0, 2, 3, 1).reshape(self.out_channels, kh * kw * C)  # [out, (dy,dx,c)]
+        out = torch.addmm(self.bias, cols, wt.t()) if self.bias is not None else cols @ wt.t()
+        return out.reshape(B, oh, ow, self.out_channels).permute(0, 3, 1, 2)
+
+
 def _pack_rows(tok):
     """Exact row key of a [B, L] token tensor (values < 32): 12 five-bit tokens per int64."""
     B, L = tok.shape
@@ -56,6 +77,7 @@ class CustomExtractor(nn.Module):
         self.n_frames_stack = n_frames_stack
         self.mission_cache = mission_cache
         self.gru_chunk = 16384          # MIOpen's RNN rejects very large batches (miopenStatusBadParm)
+        self.aten_gru = False
         self.gru = False
         ext = {}
         total = 0
@@ -64,7 +86,7 @@ class CustomExtractor(nn.Module):
                 continue
             seq = nn.Sequential()
             for i, (name, params) in enumerate(arch[key]):
-                cls = getattr(nn, name)
+                cls = Conv2dGemm if name == "Conv2d" else getattr(nn, name)
                 if params:
                     params = [list(p) if isinstance(p, (list, tuple)) else p for p in params]
                     if i == 0 and name != "Embedding":
@@ -86,7 +108,10 @@ class CustomExtractor(nn.Module):
 
     def _mission(self, seq, tok):
         if self.gru:
-            _, h = seq(tok)
+            # aten_gru: ATen's per-step fused cell instead of MIOpen's RNN (measured slower
+            # on MI355X at these shapes; kept as a switch)
+            with torch.backends.cudnn.flags(enabled=not self.aten_gru):
+                _, h = seq(tok)
             return h[-1]
         return seq(tok)
 
@@ -119,7 +144,7 @@ class CustomExtractor(nn.Module):
 
 def _init_weights(module, gain=1.0):
     """CustomPPOPolicy.init_weights (policies.py:245-255)."""
-    if isinstance(module, nn.Conv2d):
+    if isinstance(module, nn.Conv2d):                  # (Conv2dGemm is an nn.Conv2d)
         nn.init.orthogonal_(module.weight, gain=gain)
         if module.bias is not None:
             module.bias.data.fill_(0.0)

@@ -240,3 +240,20 @@ def test_rollout_collector_matches_sb3_loop():
     np.testing.assert_allclose(buf.advantages.cpu().numpy(), want_a, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(buf.returns.cpu().numpy(), want_r, rtol=1e-5, atol=1e-5)
     eng.poll_error()
+
+
+def test_conv2d_gemm_equals_conv2d():
+    from mgx.policy import Conv2dGemm
+    torch.manual_seed(4)
+    for cin, cout, k in ((12, 16, 2), (16, 32, 2), (32, 64, 2)):
+        ref = torch.nn.Conv2d(cin, cout, [k, k])
+        mine = Conv2dGemm(cin, cout, [k, k])
+        mine.load_state_dict(ref.state_dict())
+        x = torch.randn(5, cin, 7 if cin == 12 else 3, 7 if cin == 12 else 3, requires_grad=True)
+        x2 = x.detach().clone().requires_grad_(True)
+        y1, y2 = ref(x), mine(x2)
+        assert torch.allclose(y1, y2, atol=1e-5)
+        y1.square().sum().backward()
+        y2.square().sum().backward()
+        assert torch.allclose(x.grad, x2.grad, atol=1e-4)
+        assert torch.allclose(ref.weight.grad, mine.weight.grad, atol=1e-4)
