@@ -24,6 +24,7 @@ removes the dominant GRU cost at large N; gradients flow through the gather
 floating-point summation order.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -39,14 +40,17 @@ OBS_KEYS = ("direction", "image", "mission")          # observation-space (Dict)
 
 
 class Conv2dGemm(nn.Conv2d):
-    """nn.Conv2d (same parameters, init and state_dict) computed as ONE GEMM over the
-    whole batch: the kh*kw shifted views are concatenated along channels (im2col
-    without a per-sample loop; ATen's unfold and MIOpen's GEMM algorithms launch per
-    sample at batch 16k+) and contracted with the weight in a single matmul.
-    Stride 1, no padding/dilation/groups (the reference's convs); else nn.Conv2d."""
+    """nn.Conv2d (same parameters, init and state_dict) that can compute as ONE GEMM
+    over the whole batch: the kh*kw shifted views concatenated along channels (im2col
+    without a per-sample loop) and contracted with the weight in a single matmul.
+    Off by default (MGX_CONV_GEMM=1 enables it): MIOpen's own algorithms measured
+    faster for the PPO update at minibatch 65,536.  Stride 1, no padding/dilation/
+    groups (the reference's convs); anything else is plain nn.Conv2d."""
+
+    enabled = os.environ.get("MGX_CONV_GEMM", "0") == "1"   # MIOpen measured faster at batch 64k
 
     def forward(self, x):
-        if (self.padding_mode != "zeros" or self.groups != 1 or tuple(self.stride) != (1, 1)
+        if (not self.enabled or self.padding_mode != "zeros" or self.groups != 1 or tuple(self.stride) != (1, 1)
                 or tuple(self.dilation) != (1, 1) or any(self.padding)):
             return super().forward(x)
         B, C, H, W = x.shape
