@@ -245,6 +245,7 @@ def test_rollout_collector_matches_sb3_loop():
 def test_conv2d_gemm_equals_conv2d():
     from mgx.policy import Conv2dGemm
     torch.manual_seed(4)
+    Conv2dGemm.enabled = True
     for cin, cout, k in ((12, 16, 2), (16, 32, 2), (32, 64, 2)):
         ref = torch.nn.Conv2d(cin, cout, [k, k])
         mine = Conv2dGemm(cin, cout, [k, k])
@@ -257,3 +258,4 @@ def test_conv2d_gemm_equals_conv2d():
         y2.square().sum().backward()
         assert torch.allclose(x.grad, x2.grad, atol=1e-4)
         assert torch.allclose(ref.weight.grad, mine.weight.grad, atol=1e-4)
+    Conv2dGemm.enabled = False
