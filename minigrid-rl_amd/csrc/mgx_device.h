@@ -212,8 +212,8 @@ __device__ __forceinline__ void pcg_seed(Pcg &p, uint64_t seed) {
 // slots, bit 5 of every slot a zero guard): 5x denser than the words, and a SWAR
 // compare tests ten candidate words at once (see randbelow).
 constexpr int MT_FIELDS = 10;       // words per packed group
-constexpr int MT_WG = 32;           // groups per lane-private LDS window (320 words)
-constexpr int WIN_STRIDE = 66;      // dwords per lane window row: 8-B aligned, 2-way banked for b64
+constexpr int MT_WG = 16;           // groups per lane-private LDS window (160 words)
+constexpr int WIN_STRIDE = 34;      // dwords per lane window row: 8-B aligned, 2-way banked for b64
 constexpr uint64_t MT_REP = 0x041041041041041ull;   // 1 in every 6-bit slot of ten
 constexpr uint64_t MT_LOW60 = (1ull << 60) - 1ull;
 constexpr int MAX_OBJS = 32;

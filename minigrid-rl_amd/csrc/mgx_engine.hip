@@ -60,7 +60,8 @@ struct KParams {
     int terminal_mode, mission64, fast_roll;
     // pre-generated episode ring (see mgx_refill_kernel)
     uint8_t *ring_grid;     // [N][D][GS]
-    uint4 *ring_hdr;        // [N][D]   {ax|ay<<8|dir<<16|tx<<24, ty|ta<<8|mission<<16, livelocks, 0}
+    uint4 *ring_hdr;        // [N][D][3] {ax|ay<<8|dir<<16|tx<<24, ty|ta<<8|mission<<16, livelocks, 0},
+                            //           then the mission's 32 tokens (the step kernel's pop needs no lookup)
     uint4 *ring_rng;        // [N][D][2] RNG snapshot after that episode's generation
     uint4 *cur_rng;         // [N][2]   RNG snapshot after the current episode's generation
     // SPSC ring indices (mod 256; D is a power of two <= 128):
@@ -77,6 +78,7 @@ struct KParams {
     int cap;                // episodes an env produces per epoch beyond what the invariant needs (<0: fill to D)
     int initial_fill;       // this refill launch is mgx_reset's (fill every ring to 2K)
     int reset_mode;         // mgx_reset: 0 first (seeded, MT cursor 0), 1 seeded, 2 unseeded
+    int stagger;            // diagnostics (env MGX_STAGGER): odd step workgroups start this many clocks late
 };
 
 struct KOut {
@@ -167,6 +169,24 @@ __device__ __forceinline__ void write_mission_chunk(void *mis, int mission64, in
     } else {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (tok) v = reinterpret_cast<const uint4 *>(tok)[c];
+        reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(mis) + (e * n_stack + s) * 32)[c] = v;
+    }
+}
+
+// Same, tokens given as two 16-byte halves (lane-linear LDS staging of the step kernel).
+__device__ __forceinline__ void write_mission_chunk2(void *mis, int mission64, int64_t e, int n_stack, int s, int c,
+                                                     const uint8_t *lo, const uint8_t *hi, bool zeros) {
+    if (mission64) {
+        longlong2 v = make_longlong2(0, 0);
+        if (!zeros) {
+            const uint8_t *h = c < 8 ? lo : hi;
+            const int j = (2 * c) & 15;
+            v.x = h[j]; v.y = h[j + 1];
+        }
+        reinterpret_cast<longlong2 *>(reinterpret_cast<int64_t *>(mis) + (e * n_stack + s) * 32)[c] = v;
+    } else {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (!zeros) v = *reinterpret_cast<const uint4 *>(c == 0 ? lo : hi);
         reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(mis) + (e * n_stack + s) * 32)[c] = v;
     }
 }
@@ -392,13 +412,19 @@ __device__ __forceinline__ void render_block(const uint8_t *s_grid, uint8_t *s_f
 // runs right after on the same stream.  Keeping the generator out of this
 // kernel keeps it register-light (high occupancy hides its memory latency).
 template <typename ActT>
-__global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut o, const ActT *__restrict__ actions) {
+__global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, KOut o, const ActT *__restrict__ actions) {
     extern __shared__ __align__(16) uint8_t smem[];
     // fast path (n_stack == 4): smem = frame rows [64][148] (new frame at bytes 1..147);
     // staged path: smem = image stacks [64][IMG] (new frame in slot 0 of a row).
     const bool fast = p.fast_roll;
     uint8_t *s_stk = smem;
     uint8_t *s_grid = smem + p.stk_step;         // grids [64][GSL]
+    uint8_t *s_pgrid = s_grid + p.grid_lds;      // popped grids, staged [GS/16][64 lanes][16 B]
+    // popped ring slot header + RNG snapshot (LDS-DMA destinations are lane-linear; kept in the
+    // dynamic segment: hipcc 7.2 emitted no M0 setup for a static __shared__ destination)
+    uint4 *s_phdr = reinterpret_cast<uint4 *>(s_pgrid + BLOCK_ENVS * p.GS);
+    uint4 *s_tokA = s_phdr + BLOCK_ENVS;         // per lane: mission tokens 0..15 (of the mission
+    uint4 *s_tokB = s_tokA + BLOCK_ENVS;         // whose stack this step writes), tokens 16..31
     const int IMG = p.img_bytes;
     const int FSTRIDE = fast ? FROW : IMG, FOFF = fast ? 1 : 0;
     __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params ax | ay<<8 | dir<<16 | carry<<24
@@ -408,8 +434,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     __shared__ uint8_t s_dlist[BLOCK_ENVS];      // envs that popped a new episode (render + mission lists)
     __shared__ uint8_t s_flist[BLOCK_ENVS];      // envs whose mission stack is still filling
     __shared__ uint8_t s_fslot[BLOCK_ENVS];      // ... and the slot that flips 0 -> tokens
-    __shared__ uint8_t s_mid[BLOCK_ENVS];        // mission id whose tokens those writes use
+    __shared__ uint32_t s_rp2[BLOCK_ENVS];       // render params of the popped episodes' first frames
     __shared__ int s_nd, s_npop, s_nf;
+    __shared__ unsigned long long s_dmask, s_tmask;   // done / terminal-written envs as bit masks
     __shared__ unsigned long long s_ll;
 
     const int tid = threadIdx.x;
@@ -417,9 +444,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     const int ne = (int)min<int64_t>(BLOCK_ENVS, p.n - e0);
     const int S = p.S;
     if (tid == 0) s_ll = 0;
+    if (p.stagger && (blockIdx.x & 1)) {          // diagnostics: desynchronise the workgroups' phases
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)p.stagger) __builtin_amdgcn_s_sleep(8);
+    }
 #ifdef MGX_STAMPS
     const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-    unsigned long long ts1 = 0, ts2 = 0, tsA = 0, tsB = 0;
+    unsigned long long ts1 = 0, ts2 = 0, tsA = 0, tsB = 0, tsC = 0;
 #endif
 
     // ---- phase 1: issue every independent load up front --------------------------
@@ -427,11 +458,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     EnvState st;
     int a = 0;
     uint4 odir = make_uint4(0, 0, 0, 0);          // old direction stack (n_stack == 4: one uint4)
+    uint8_t rhead = 0, rpub = 0;                  // this env's ring position and published end
     if (tid < ne) {
         st = p.state[e0 + tid];
         a = (int)actions[e0 + tid];
         if (p.n_stack == 4) odir = reinterpret_cast<const uint4 *>(o.dir)[e0 + tid];
+        if (p.D > 0) { rhead = p.ring_head[e0 + tid]; rpub = p.ring_pub[e0 + tid]; }
     }
+
     // (b) fast roll: the old image-stack dwords this lane's output quads need, into registers
     constexpr int DW = FRAME_DW4;                                                     // 147
     constexpr int MAXQ = (BLOCK_ENVS * DW / 4 + BLOCK_THREADS - 1) / BLOCK_THREADS;  // 10
@@ -507,7 +541,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     // above), so these stores drain while wave 0 runs the step logic and the block
     // renders.  Pass 2 (phase 3) writes what depends on this step: the new frame
     // (j >= 110) and the zeroed old part of done envs.
-    if (fast) {
+    // Waves 1-3 store now; wave 0 (the env lanes) stores its share after its ring pop,
+    // whose loads must not queue behind stores.
+    auto roll_pass1 = [&]() {
         uint32_t *g32 = reinterpret_cast<uint32_t *>(o.img + e0 * (int64_t)IMG);
         uint4 *g128 = reinterpret_cast<uint4 *>(g32);
 #pragma unroll
@@ -534,7 +570,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
             }
         }
         // tail dword of a partial block: written in pass 2 only
-    }
+    };
+    if (fast && tid >= BLOCK_ENVS) roll_pass1();
 
     // ---- phase 2a: one lane per env: MiniGridEnv.step + PlaygroundEnv.step
     uint32_t my_err = 0;
@@ -619,6 +656,67 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
             }
         }
         done = term || trunc;
+        const bool tw = done && (p.terminal_mode == MGX_TERMINAL_ALL ||
+                                 (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term));
+        if (tw) {                                      // stacked terminal_observation: dir + mission
+            // (rare; before the pop rewrites this env's direction row)
+            const int frames = min((int)st.frames + 1, p.n_stack);
+            if (p.n_stack == 4)
+                reinterpret_cast<uint4 *>(o.t_dir)[e] = make_uint4(odir.y, odir.z, odir.w, 1u << (8 * dir));
+            else
+                dir_stack_roll(o.dir, o.t_dir, e, p.n_stack, dir);
+            write_mission_stack(o.t_mis, p.mission64, e, p.n_stack, frames, p.mtok + st.mission_id * 32);
+        }
+        // SubprocVecEnv auto-reset: pop the next pre-generated episode.  Its loads go out
+        // before this lane's other stores (LDS-DMA, no registers).
+        const bool avail = done && p.D > 0 && (uint8_t)(rpub - rhead) != 0;
+        const bool filling = !done && st.frames < p.n_stack;
+        uint4 rng0 = make_uint4(0, 0, 0, 0), rng1 = rng0;
+        if (avail) {
+            const int64_t slot = e * p.D + (rhead & (p.D - 1));
+            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot, s_phdr, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 1, s_tokA, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 2, s_tokB, 16, 0, 0);
+            const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
+            for (int c = 0; c < (p.GS >> 4); c++)          // popped grid -> staging [chunk][lane]
+                __builtin_amdgcn_global_load_lds(gsrc + c, s_pgrid + c * (BLOCK_ENVS * 16), 16, 0, 0);
+            rng0 = p.ring_rng[2 * slot];
+            rng1 = p.ring_rng[2 * slot + 1];
+        } else if (filling) {                               // tokens of the mission that stays
+            const uint4 *t = reinterpret_cast<const uint4 *>(p.mtok + st.mission_id * 32);
+            __builtin_amdgcn_global_load_lds(t, s_tokA, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(t + 1, s_tokB, 16, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0);                      // one round trip, nothing else outstanding
+        if (avail) {
+            const uint4 h = s_phdr[tid];
+            p.cur_rng[2 * e] = rng0;
+            p.cur_rng[2 * e + 1] = rng1;
+            new_head = (int)(uint8_t)(rhead + 1);   // published after a barrier, loads consumed
+            const int nax = h.x & 0xFF, nay = (h.x >> 8) & 0xFF, ndir = (h.x >> 16) & 0xFF;
+            const uint8_t mid = (uint8_t)(h.y >> 16);
+            EnvState ns;
+            ns.ax = (uint8_t)nax; ns.ay = (uint8_t)nay; ns.dir = (uint8_t)ndir; ns.carry = 0;
+            ns.step_count = 0; ns.reward_step = (int16_t)rs;          // survives the reset (Q2)
+            ns.tx = (uint8_t)(h.x >> 24); ns.ty = (uint8_t)h.y; ns.target_action = (uint8_t)(h.y >> 8);
+            ns.mission_id = mid;
+            ns.mission_done = (uint8_t)mdone; ns.frames = 1; ns.flags = 0; ns.pad = 0;
+            p.state[e] = ns;
+            s_rp2[tid] = (uint32_t)nax | ((uint32_t)nay << 8) | ((uint32_t)ndir << 16);
+            dir_stack_fresh(o.dir, e, p.n_stack, ndir);
+            if (o.livelock) o.livelock[e] = (int)h.z;
+            dirty = true;
+            popped = true;
+            if (h.z) atomicAdd(&s_ll, (unsigned long long)h.z);
+        } else if (done && p.D > 0) {
+            my_err |= MGX_DEVERR_RING_EMPTY;   // cannot happen (refill production rule)
+        } else if (done) {
+            // no ring: mgx_fixup_kernel generates this env's episode inline.  Keep the
+            // episode-spanning flags (Q2) in the state it will complete.
+            st.reward_step = (int16_t)rs; st.mission_done = (uint8_t)mdone;
+            p.state[e] = st;
+            p.fix_list[atomicAdd(p.fix_count, 1u)] = (uint32_t)e;
+        }
         o.reward[e] = (float)rew;
         if (o.reward64) o.reward64[e] = rew;
         o.term[e] = term;
@@ -632,10 +730,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
                 reinterpret_cast<uint4 *>(o.dir)[e] = make_uint4(odir.y, odir.z, odir.w, 1u << (8 * dir));
             else
                 dir_stack_roll(o.dir, o.dir, e, p.n_stack, dir);
-            if (st.frames < p.n_stack) {               // stack still filling: one slot flips 0 -> mission
+            if (filling) {                             // stack still filling: one slot flips 0 -> mission
                 fill = true;
                 s_fslot[tid] = (uint8_t)(p.n_stack - frames);
-                s_mid[tid] = st.mission_id;
             }
             st.ax = (uint8_t)ax; st.ay = (uint8_t)ay; st.dir = (uint8_t)dir; st.carry = carry;
             st.step_count = (uint16_t)sc; st.reward_step = (int16_t)rs; st.mission_done = (uint8_t)mdone;
@@ -644,16 +741,18 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
             if (o.livelock) o.livelock[e] = 0;
         }
         s_done[tid] = done;
-        s_term[tid] = done && (p.terminal_mode == MGX_TERMINAL_ALL ||
-                               (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term));
+        s_term[tid] = tw;
     } else if (tid < BLOCK_ENVS) {
         s_done[tid] = 0;
         s_term[tid] = 0;
     }
-    if (tid < BLOCK_ENVS) {                            // wave 0: ballot compaction of the fill list
-        const unsigned long long fm = __ballot(fill), dm = __ballot(done);
+    if (fast && tid < BLOCK_ENVS) roll_pass1();        // wave 0's share of the early roll stores
+    if (tid < BLOCK_ENVS) {                            // wave 0: ballot compaction of the lists
+        const unsigned long long fm = __ballot(fill), dm = __ballot(done), pm = __ballot(popped);
+        const unsigned long long tm = __ballot(tid < ne && s_term[tid]);
         if (fill) s_flist[__popcll(fm & __lanemask_lt())] = (uint8_t)tid;
-        if (tid == 0) { s_nf = __popcll(fm); s_nd = __popcll(dm); }
+        if (popped) s_dlist[__popcll(pm & __lanemask_lt())] = (uint8_t)tid;
+        if (tid == 0) { s_nf = __popcll(fm); s_nd = __popcll(dm); s_npop = __popcll(pm); s_dmask = dm; s_tmask = tm; }
     }
     __syncthreads();
 
@@ -667,98 +766,49 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
     tsB = __builtin_amdgcn_s_memtime();
 #endif
 
-    // ---- phase 2c: done envs: terminal_observation, then auto-reset from the ring
+    // ---- phase 2c: done envs: newest slot of the terminal stack, popped grids into place
     const int nd = s_nd;
     if (nd) {
         if (tid < ne && done) {
-            const int64_t e = e0 + tid;
-            const uint8_t *fr = s_stk + tid * FSTRIDE + FOFF;    // terminal frame
-            const int frames = min((int)st.frames + 1, p.n_stack);
-            if (p.terminal_mode == MGX_TERMINAL_ALL || (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term)) {
-                // re-stacked like VecFrameStack (rare -> per-lane writes): older frames, then the terminal one
+            if (s_term[tid]) {                         // the terminal frame (older frames: phase 3)
+                const int64_t e = e0 + tid;
                 uint8_t *t = o.t_img + e * (int64_t)IMG;
-                if (!fast) {             // fast path: the quad owners write the older frames in phase 3
+                const uint8_t *fr = s_stk + tid * FSTRIDE + FOFF;
+                if (!fast) {
                     const uint8_t *old = s_stk + tid * IMG;
                     for (int off = 0; off < IMG - FRAME; off++) t[off] = old[off + FRAME];
                 }
                 for (int k = 0; k < FRAME; k++) t[IMG - FRAME + k] = fr[k];
-                if (p.n_stack == 4)
-                    reinterpret_cast<uint4 *>(o.t_dir)[e] = make_uint4(odir.y, odir.z, odir.w, 1u << (8 * dir));
-                else
-                    dir_stack_roll(o.dir, o.t_dir, e, p.n_stack, dir);
-                write_mission_stack(o.t_mis, p.mission64, e, p.n_stack, frames, p.mtok + st.mission_id * 32);
             }
-            // SubprocVecEnv auto-reset: env.reset() (unseeded): pop the next pre-generated episode
-            uint8_t *g = s_grid + tid * p.GSL;
-            const uint8_t head = p.D > 0 ? p.ring_head[e] : 0;
-            const bool avail = p.D > 0 && (uint8_t)(p.ring_pub[e] - head) != 0;
-            if (avail) {
-                const int64_t slot = e * p.D + (head & (p.D - 1));
-                const uint4 h = p.ring_hdr[slot];
-                const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
+            if (popped) {                              // staged popped grid -> this env's grid row
+                uint32_t *d = reinterpret_cast<uint32_t *>(s_grid + tid * p.GSL);
                 for (int c = 0; c < (p.GS >> 4); c++) {
-                    const uint4 v = gsrc[c];
-                    uint32_t *d = reinterpret_cast<uint32_t *>(g + c * 16);
-                    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+                    const uint32_t *q = reinterpret_cast<const uint32_t *>(s_pgrid + c * (BLOCK_ENVS * 16) + tid * 16);
+                    d[4 * c] = q[0]; d[4 * c + 1] = q[1]; d[4 * c + 2] = q[2]; d[4 * c + 3] = q[3];
                 }
-                p.cur_rng[2 * e] = p.ring_rng[2 * slot];
-                p.cur_rng[2 * e + 1] = p.ring_rng[2 * slot + 1];
-                new_head = (int)(uint8_t)(head + 1);   // published after the barrier below, once
-                                                         // this slot's loads have been consumed
-                const int nax = h.x & 0xFF, nay = (h.x >> 8) & 0xFF, ndir = (h.x >> 16) & 0xFF;
-                const uint8_t mid = (uint8_t)(h.y >> 16);
-                EnvState ns;
-                ns.ax = (uint8_t)nax; ns.ay = (uint8_t)nay; ns.dir = (uint8_t)ndir; ns.carry = 0;
-                ns.step_count = 0; ns.reward_step = (int16_t)rs;          // survives the reset (Q2)
-                ns.tx = (uint8_t)(h.x >> 24); ns.ty = (uint8_t)h.y; ns.target_action = (uint8_t)(h.y >> 8);
-                ns.mission_id = mid;
-                ns.mission_done = (uint8_t)mdone; ns.frames = 1; ns.flags = 0; ns.pad = 0;
-                p.state[e] = ns;
-                s_rp[tid] = (uint32_t)nax | ((uint32_t)nay << 8) | ((uint32_t)ndir << 16);
-                dir_stack_fresh(o.dir, e, p.n_stack, ndir);
-                s_mid[tid] = mid;                                 // fresh mission stack: block writer below
-                if (o.livelock) o.livelock[e] = (int)h.z;
-                dirty = true;
-                popped = true;
-                if (h.z) atomicAdd(&s_ll, (unsigned long long)h.z);
-            } else if (p.D > 0) {
-                // cannot happen while refill_every <= D/2 (each step pops at most one episode)
-                my_err |= MGX_DEVERR_RING_EMPTY;
-            } else {
-                // no ring: mgx_fixup_kernel generates this env's episode inline.  Keep the
-                // episode-spanning flags (Q2) in the state it will complete.
-                st.reward_step = (int16_t)rs; st.mission_done = (uint8_t)mdone;
-                p.state[e] = st;
-                p.fix_list[atomicAdd(p.fix_count, 1u)] = (uint32_t)e;
             }
-        }
-        if (tid < BLOCK_ENVS) {                        // wave 0: ballot compaction of the pop list
-            const unsigned long long pm = __ballot(popped);
-            if (popped) s_dlist[__popcll(pm & __lanemask_lt())] = (uint8_t)tid;
-            if (tid == 0) s_npop = __popcll(pm);
         }
         __syncthreads();
         // first frames of the new episodes -> frame rows (phase 3 zero-fills the older slots)
-        render_block(s_grid, s_stk, s_rp, s_dlist, s_npop, S, p.GSL, FSTRIDE, FOFF);
-    } else if (tid == 0) {
-        s_npop = 0;
+        render_block(s_grid, s_stk, s_rp2, s_dlist, s_npop, S, p.GSL, FSTRIDE, FOFF);
     }
     __syncthreads();
     // mission stacks, block-cooperative and coalesced: fresh stacks of popped envs
     // (zeros + tokens in the newest slot), then the one flipping slot of filling envs
     {
         const int K = p.n_stack, CPS = p.mission64 ? 16 : 2, per = K * CPS;
+        const uint8_t *tA = reinterpret_cast<const uint8_t *>(s_tokA), *tB = reinterpret_cast<const uint8_t *>(s_tokB);
         const int tot_d = s_npop * per;
         for (int w = tid; w < tot_d; w += BLOCK_THREADS) {
             const int i = w / per, j = w - i * per;
             const int le = s_dlist[i], sl = j / CPS, c = j - sl * CPS;
-            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk(o.mis, p.mission64, e0 + le, K, sl, c, sl == K - 1 ? p.mtok + s_mid[le] * 32 : nullptr);
+            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk2(o.mis, p.mission64, e0 + le, K, sl, c, tA + le * 16, tB + le * 16, sl != K - 1);
         }
         const int tot_f = s_nf * CPS;
         for (int w = tid; w < tot_f; w += BLOCK_THREADS) {
             const int i = w / CPS, c = w - i * CPS;
             const int le = s_flist[i];
-            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk(o.mis, p.mission64, e0 + le, K, s_fslot[le], c, p.mtok + s_mid[le] * 32);
+            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk2(o.mis, p.mission64, e0 + le, K, s_fslot[le], c, tA + le * 16, tB + le * 16, false);
         }
     }
     if (tid < BLOCK_ENVS) s_dirty[tid] = dirty;
@@ -778,31 +828,34 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         // The old dwords were loaded into registers in phase 1, before any store: in place, no hazard.
         const uint32_t *f32 = reinterpret_cast<const uint32_t *>(s_stk);
         uint4 *g128 = reinterpret_cast<uint4 *>(o.img + e0 * (int64_t)IMG);
+        const unsigned long long dmask = s_dmask, tmask = s_tmask;    // wave-uniform
 #pragma unroll
         for (int r = 0; r < MAXQ; r++) {
             const int q = r * BLOCK_THREADS + tid, k = 4 * q;
-            if (q < nq) {
+            const int e0q = k / DW, j0 = k - e0q * DW;
+            // envs this quad touches (it straddles at most one row boundary)
+            const unsigned long long qm = (3ull << e0q) & ((j0 >= DW - 3) ? ~0ull : (1ull << e0q));
+            const bool need = q < nq && (j0 >= 107 || (dmask & qm) || (tmask & qm));
+            if (need) {                              // else pass 1 already stored this quad as-is
                 const uint32_t src[5] = {qa[r].x, qa[r].y, qa[r].z, qa[r].w, qb[r]};
-                int e = k / DW, j = k - e * DW;
+                int e = e0q, j = j0;
                 uint32_t w[4];
-                bool need = false;                   // pass 1 already stored this quad as-is?
 #pragma unroll
                 for (int t = 0; t < 4; t++) {
-                    const bool dn = s_done[e];
-                    need |= dn || j >= 110;
+                    const bool dn = (dmask >> e) & 1ull;
                     uint32_t out;
                     if (j <= 109) out = dn ? 0u : __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
                     else if (j == 110) out = (f32[e * (FROW / 4)] & 0xFFFFFF00u) | (dn ? 0u : (src[t] >> 24));
                     else out = f32[e * (FROW / 4) + (j - 110)];
                     w[t] = out;
-                    if (s_term[e]) {                 // terminal_observation: the older frames (rare)
+                    if ((tmask >> e) & 1ull) {       // terminal_observation: the older frames (rare)
                         uint8_t *trow = o.t_img + (e0 + e) * (int64_t)IMG;
                         if (j <= 109) reinterpret_cast<uint32_t *>(trow)[j] = __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
                         else if (j == 110) trow[4 * 110] = (uint8_t)(src[t] >> 24);   // old byte 587
                     }
                     if (++j == DW) { j = 0; e++; }
                 }
-                if (!(MGX_DIAG_SKIP & 2)) if (need) stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
+                if (!(MGX_DIAG_SKIP & 2)) stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
             }
         }
         // tail dword (partial last block whose row count is not a multiple of 4): its old
@@ -837,6 +890,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         }
     }
 
+#ifdef MGX_STAMPS
+    tsC = __builtin_amdgcn_s_memtime();
+#endif
     // ---- phase 5: write back grids that changed (moves, pickups, resets)
     if (!(MGX_DIAG_SKIP & 16)) grid_copy_out(p.grid + e0 * p.GS, s_grid, ne, p.GS, p.GSL, s_dirty);
     if (tid == 0) {
@@ -850,10 +906,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_step_kernel(KParams p, KOut
         atomicAdd(&p.counters[5], tsA - ts1);   // phase 2a: step logic
 #if MGX_STAMPS == 2
         atomicAdd(&p.counters[6], tsB - tsA);   // phase 2b: render
+        atomicAdd(&p.counters[7], ts4 - ts2);   // phase 3+5: stack roll + grid write-back
+#elif MGX_STAMPS == 3
+        atomicAdd(&p.counters[6], tsC - ts2);   // phase 3: roll pass 2
+        atomicAdd(&p.counters[7], ts4 - tsC);   // phase 5: grid write-back, ring heads, stats
 #else
         atomicAdd(&p.counters[6], ts2 - tsA);   // phase 2b+2c: render, done envs, ring pops, render
-#endif
         atomicAdd(&p.counters[7], ts4 - ts2);   // phase 3+5: stack roll + grid write-back
+#endif
 #endif
     }
 }
@@ -975,7 +1035,9 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
                     const uint32_t *q = reinterpret_cast<const uint32_t *>(G.g + c * 16);
                     dst[c] = make_uint4(q[0], q[1], q[2], q[3]);
                 }
-                p.ring_hdr[slot] = pack_hdr(G, R);
+                p.ring_hdr[3 * slot] = pack_hdr(G, R);
+                p.ring_hdr[3 * slot + 1] = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[0];
+                p.ring_hdr[3 * slot + 2] = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[1];
                 rng_snapshot(G, p.ring_rng + 2 * slot);
                 tail++;
             }
@@ -1240,6 +1302,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     {
         const char *sv = std::getenv("MGX_SERIAL_REFILL");
         h->serial_refill = sv && sv[0] == '1';
+        const char *st = std::getenv("MGX_STAGGER");
+        h->kp.stagger = st ? std::atoi(st) : 0;
     }
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 24;
     h->cfg.mt_table_words = (h->cfg.mt_table_words + MT_FIELDS - 1) / MT_FIELDS * MT_FIELDS;
@@ -1264,7 +1328,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     }
     const int D = h->cfg.ring_depth;
     {
-        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 16, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 3 + 64};
+        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 48, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 3 + 64};
         for (int i = 0; i < 5; i++) {
             hipError_t e = hipMalloc(&h->allocs[7 + i], rs[i] ? rs[i] : 16);
             if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, std::string("hipMalloc ring: ") + hipGetErrorString(e)));
@@ -1355,7 +1419,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.cap = h->cfg.refill_cap;
     p.initial_fill = 0;
     p.mission64 = cfg->mission_int64;
-    h->lds_step = (size_t)p.stk_step + (size_t)p.grid_lds;
+    h->lds_step = (size_t)p.stk_step + (size_t)p.grid_lds + (size_t)BLOCK_ENVS * (GS + 48);   // + popped slot staging
     h->lds_reset = (size_t)p.stk_lds + (size_t)p.grid_lds;
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));

@@ -2,7 +2,7 @@ import sys, time, json
 import os; sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'minigrid-rl_amd')]
 import torch
 from mgx import MgxEngine
-n = 65536
+n = int(os.environ.get("N", 65536))
 import sys as _s
 e = MgxEngine(problem="multi", mission=5, size=8, n_envs=n)
 acts = torch.randint(0, 7, (256, n), device="cuda", dtype=torch.int32)
