@@ -118,6 +118,12 @@ __device__ __forceinline__ void grid_copy_out(uint8_t *g, const uint8_t *lds, in
     }
 }
 
+// A value every lane holds the same copy of (read from LDS) -> SGPRs
+__device__ __forceinline__ unsigned long long wave_uniform64(unsigned long long v) {
+    return ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
 // Image-stack stores (diagnostic switch: -DMGX_NT_STACK = non-temporal)
 __device__ __forceinline__ void stk_store(uint4 *p, uint4 v) {
 #ifdef MGX_NT_STACK
@@ -531,6 +537,11 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         for (int i = tid; i < n16; i += BLOCK_THREADS) dst[i] = src[i];
         for (int i = (n16 << 4) + tid; i < nbytes; i += BLOCK_THREADS) s_stk[i] = gimg[i];
     }
+    // Every phase-1 load has landed (the grid copy already drained them in issue order).
+    // Saying so explicitly matters: otherwise the waitcnt pass assumes a qa/qb load may be
+    // pending on some path and puts a vmcnt(0) before every roll quad, which then waits on
+    // the previous quad's STORES (vmcnt counts both) and serialises the whole roll.
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 #ifdef MGX_STAMPS
     ts1 = __builtin_amdgcn_s_memtime();
@@ -828,34 +839,58 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         // The old dwords were loaded into registers in phase 1, before any store: in place, no hazard.
         const uint32_t *f32 = reinterpret_cast<const uint32_t *>(s_stk);
         uint4 *g128 = reinterpret_cast<uint4 *>(o.img + e0 * (int64_t)IMG);
-        const unsigned long long dmask = s_dmask, tmask = s_tmask;    // wave-uniform
+        // block-uniform masks in SGPRs: the terminal branch below is scalar
+        const unsigned long long dmask = wave_uniform64(s_dmask), tmask = wave_uniform64(s_tmask);
 #pragma unroll
         for (int r = 0; r < MAXQ; r++) {
             const int q = r * BLOCK_THREADS + tid, k = 4 * q;
             const int e0q = k / DW, j0 = k - e0q * DW;
             // envs this quad touches (it straddles at most one row boundary)
             const unsigned long long qm = (3ull << e0q) & ((j0 >= DW - 3) ? ~0ull : (1ull << e0q));
-            const bool need = q < nq && (j0 >= 107 || (dmask & qm) || (tmask & qm));
+            const bool need = q < nq && (j0 >= 107 || (dmask & qm));
             if (need) {                              // else pass 1 already stored this quad as-is
+                // Branch-free: the 4 frame-row dwords are read together (one LDS round trip),
+                // then each output dword is a select of old / mixed / new.
                 const uint32_t src[5] = {qa[r].x, qa[r].y, qa[r].z, qa[r].w, qb[r]};
+                uint32_t fv[4];
                 int e = e0q, j = j0;
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    fv[t] = f32[e * (FROW / 4) + max(j - 110, 0)];
+                    if (++j == DW) { j = 0; e++; }
+                }
+                e = e0q; j = j0;
                 uint32_t w[4];
 #pragma unroll
                 for (int t = 0; t < 4; t++) {
                     const bool dn = (dmask >> e) & 1ull;
-                    uint32_t out;
-                    if (j <= 109) out = dn ? 0u : __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
-                    else if (j == 110) out = (f32[e * (FROW / 4)] & 0xFFFFFF00u) | (dn ? 0u : (src[t] >> 24));
-                    else out = f32[e * (FROW / 4) + (j - 110)];
-                    w[t] = out;
-                    if ((tmask >> e) & 1ull) {       // terminal_observation: the older frames (rare)
-                        uint8_t *trow = o.t_img + (e0 + e) * (int64_t)IMG;
-                        if (j <= 109) reinterpret_cast<uint32_t *>(trow)[j] = __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
-                        else if (j == 110) trow[4 * 110] = (uint8_t)(src[t] >> 24);   // old byte 587
-                    }
+                    const uint32_t old = dn ? 0u : __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
+                    const uint32_t mix = (fv[t] & 0xFFFFFF00u) | (dn ? 0u : (src[t] >> 24));
+                    w[t] = j <= 109 ? old : (j == 110 ? mix : fv[t]);
                     if (++j == DW) { j = 0; e++; }
                 }
                 if (!(MGX_DIAG_SKIP & 2)) stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
+            }
+        }
+        if (tmask) {                                 // terminal_observation: the older frames (rare)
+#pragma unroll
+            for (int r = 0; r < MAXQ; r++) {
+                const int q = r * BLOCK_THREADS + tid, k = 4 * q;
+                const int e0q = k / DW, j0 = k - e0q * DW;
+                const unsigned long long qm = (3ull << e0q) & ((j0 >= DW - 3) ? ~0ull : (1ull << e0q));
+                if (q < nq && (tmask & qm)) {
+                    const uint32_t src[5] = {qa[r].x, qa[r].y, qa[r].z, qa[r].w, qb[r]};
+                    int e = e0q, j = j0;
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        if ((tmask >> e) & 1ull) {
+                            uint8_t *trow = o.t_img + (e0 + e) * (int64_t)IMG;
+                            if (j <= 109) reinterpret_cast<uint32_t *>(trow)[j] = __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
+                            else if (j == 110) trow[4 * 110] = (uint8_t)(src[t] >> 24);   // old byte 587
+                        }
+                        if (++j == DW) { j = 0; e++; }
+                    }
+                }
             }
         }
         // tail dword (partial last block whose row count is not a multiple of 4): its old
