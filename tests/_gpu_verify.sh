@@ -1,0 +1,20 @@
+#!/bin/bash
+# One gpurun call: GPU parity tests -> smoke -> default bench -> rocprof kernel stats of the bench.
+# Every GPU step has its own time limit; the first failing step ends the call.
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -rf > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+tail -3 $O/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 400 python bench.py > $O/bench.json 2>$O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+python3 -c "
+import csv
+for r in list(csv.DictReader(open('$O/prof/run_kernel_stats.csv')))[:6]:
+    print(r['Name'][:60], r['Calls'], r['AverageNs'], r['Percentage'])
+"
