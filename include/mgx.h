@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MGX_ABI_VERSION 1
+#define MGX_ABI_VERSION 2
 
 /* Live-lock cap (engine policy; the reference hangs): a
  * reset attempt may consume at most this many MT19937 words; the attempt that
@@ -68,12 +68,14 @@ typedef enum { MGX_TERMINAL_NONE = 0, MGX_TERMINAL_TRUNCATED = 1, MGX_TERMINAL_A
 
 typedef struct mgx_config {
     int32_t problem;           /* mgx_problem; `env.problem` */
-    int32_t mission;           /* `env.mission`: 0 'go to', 1 'toggle', 2 'pick up', 5 'go to goal'; -1 = None */
+    int32_t mission;           /* `env.mission` (problem multi): 0 'go to', 1 'toggle', 2 'pick up',
+                                  5 'go to goal'; -1 = None */
     int32_t size;              /* `env.size` (5..16); max_steps = size^2 (custom_env.py:114) */
     int32_t num_objects;       /* `env.num_objects` */
-    int32_t see_through_walls; /* must be 1 (process_vis path not built) */
+    int32_t see_through_walls; /* `env.see_through_walls`; 0 = minigrid Grid.process_vis occlusion */
     int32_t all_doors_open;    /* `env.all_doors_open` */
-    int32_t obstacles;         /* must be 0 (every shipped config) */
+    int32_t obstacles;         /* `env.obstacles`: floor((size-2)^2 * percent_obstacles) lava (multi) or
+                                  lava/wall (single room) cells (custom_env.py:154-172) */
     int32_t n_stack;           /* `algorithm.n_frames_stack` (1..8) */
     int64_t n_envs;            /* envs owned by this handle */
     int64_t base_seed;         /* `seed`; env i: PCG64(SeedSequence(base_seed + env_index_offset + i)), MT19937(base_seed) */
@@ -88,6 +90,7 @@ typedef struct mgx_config {
                                   <= 128; -1 = no ring: every auto-reset generated inline) */
     int32_t refill_every;      /* steps per refill epoch K (0 -> ring_depth/4; clamped to <= ring_depth/2:
                                   each epoch keeps >= K queued, and a step pops <= 1 episode) */
+    double percent_obstacles;  /* `env.percent_obstacles` (single.yaml:28: 0.05); used when obstacles */
 } mgx_config;
 
 /* Stacked observation in the layout SB3's VecFrameStack(VecTransposeImage(.))

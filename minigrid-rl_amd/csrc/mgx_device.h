@@ -9,11 +9,16 @@
 //   PlaygroundEnv._gen_grid        src/custom_env.py:122-267   -> gen_attempt()/reset_env()
 //   _generate_multi_map            src/custom_env.py:595-615   -> gen_multi()
 //   _generate_2/3/4_rooms          src/custom_env.py:617-2034  -> gen_2/3/4_rooms()
+//   _generate_full_map             src/custom_env.py:332-369   -> gen_single()
 //   _generate_{gto,gtg,open,pkp}   src/custom_env.py:371-513   -> gen_single()
+//   _generate_{drop,move}_map      src/custom_env.py:515-593   -> gen_single()
+//   obstacles (cfg.obstacles)      src/custom_env.py:154-172   -> place_obstacles()
+//   'drop' / 'move' missions       src/custom_env.py:214-256   -> gen_attempt(), move_range()
 //   next2door                      src/custom_env.py:2036-2046 -> next2door()
 //   TokenizeVocabWrapper           src/environment.py:91-112   -> host mission table
 //   Discrete2BoxWrapper            src/environment.py:144-149  -> one-hot direction stack
-// plus minigrid's MiniGridEnv.step/gen_obs/place_obj/place_agent (3P),
+// plus minigrid's MiniGridEnv.step/gen_obs/place_obj/place_agent and Grid.process_vis
+// (see_through_walls=False -> apply_vis()) (3P),
 // CPython random (_randbelow via getrandbits) and numpy PCG64/Generator.integers (A.6).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -29,6 +34,7 @@ namespace mgx {
 constexpr uint8_t CODE_EMPTY = 0x01;
 constexpr uint8_t CODE_WALL = 2 | (5 << 4);   // Wall() is grey
 constexpr uint8_t CODE_GOAL = 8 | (1 << 4);   // Goal() is green
+constexpr uint8_t CODE_LAVA = 9;              // Lava() is red (COLOR_TO_IDX 0)
 constexpr int T_EMPTY = 1, T_WALL = 2, T_DOOR = 4, T_KEY = 5, T_BALL = 6, T_BOX = 7,
               T_GOAL = 8, T_LAVA = 9, T_OPEN = 11;
 constexpr int A_LEFT = 0, A_RIGHT = 1, A_FORWARD = 2, A_PICKUP = 3, A_DROP = 4,
@@ -70,8 +76,10 @@ struct __align__(16) EnvState {
 };
 static_assert(sizeof(EnvState) == 16, "EnvState must be 16 bytes");
 
-// mission ids
+// mission ids: cmd | colour-name<<2 | type-slot<<5 for 'go to' / 'toggle' / 'pick up',
+// 3 = 'go to goal', MID_DROP = 'drop', MID_MOVE + d = 'move left/right/up/down'
 constexpr int CMD_GOTO = 0, CMD_TOGGLE = 1, CMD_PICKUP = 2, CMD_GOTOGOAL = 3;
+constexpr int MID_DROP = 128, MID_MOVE = 129;
 constexpr int TS_DOOR = 0, TS_KEY = 1, TS_BALL = 2, TS_BOX = 3;
 __device__ __forceinline__ int type_slot(int t) {
     return t == T_DOOR ? TS_DOOR : t == T_KEY ? TS_KEY : t == T_BALL ? TS_BALL : TS_BOX;
@@ -280,7 +288,7 @@ struct Gen {
     int nobjs;
     uint32_t tmask;        // bit t: an object of type t is in objs
     // config
-    int problem, cfg_mission, num_objects, all_doors_open;
+    int problem, cfg_mission, num_objects, all_doors_open, n_obstacles;
 #ifdef MGX_GEN_STAMPS
     unsigned long long *stamps;   // diagnostic build: per-section wave clocks (counters[8..])
     uint64_t tlast;
@@ -836,21 +844,39 @@ __device__ const int GTG_T[4] = {T_BOX, T_DOOR, T_KEY, T_BALL};
 __device__ const int OPN_T[2] = {T_BOX, T_DOOR};
 __device__ const int PKP_T[3] = {T_KEY, T_BOX, T_BALL};
 
-template <int NW>
-__device__ __forceinline__ int gen_single(Gen<NW> &G) {           // custom_env.py:371-513
+// EXT = the generator variant with the problems / features no shipped config uses (full, drp,
+// mov, obstacles): compiled out of the default variant so its register budget is unchanged.
+template <int NW, bool EXT>
+__device__ __forceinline__ int gen_single(Gen<NW> &G) {           // custom_env.py:332-593
     const int *types;
     int ntypes, cmd;
     bool goal = false;
-    switch (G.problem) {
-        case 2: types = GTO_T; ntypes = 4; cmd = 0; break;             // gto -> 'go to'
-        case 3: types = GTG_T; ntypes = 4; cmd = 5; goal = true; break; // gtg -> 'go to goal'
-        case 4: types = OPN_T; ntypes = 2; cmd = 1; break;             // opn -> 'toggle'
-        default: types = PKP_T; ntypes = 3; cmd = 2; break;            // pkp -> 'pick up'
+    const bool full = EXT && G.problem == 1;
+    if constexpr (EXT) {
+        switch (G.problem) {
+            case 1: types = GTO_T; ntypes = 4; cmd = -1; goal = true; break;  // full: every (type, colour)
+            case 2: types = GTO_T; ntypes = 4; cmd = 0; break;              // gto -> 'go to'
+            case 3: types = GTG_T; ntypes = 4; cmd = 5; goal = true; break;  // gtg -> 'go to goal'
+            case 4: types = OPN_T; ntypes = 2; cmd = 1; break;              // opn -> 'toggle'
+            case 6: types = GTO_T; ntypes = 4; cmd = 3; goal = true; break;  // drp -> 'drop'
+            case 7: types = GTO_T; ntypes = 4; cmd = 4; break;              // mov -> 'move <dir>'
+            default: types = PKP_T; ntypes = 3; cmd = 2; break;             // pkp -> 'pick up'
+        }
+    } else {
+        switch (G.problem) {
+            case 2: types = GTO_T; ntypes = 4; cmd = 0; break;
+            case 3: types = GTG_T; ntypes = 4; cmd = 5; goal = true; break;
+            case 4: types = OPN_T; ntypes = 2; cmd = 1; break;
+            default: types = PKP_T; ntypes = 3; cmd = 2; break;
+        }
     }
     uint32_t oc = (1u << (ntypes * 6)) - 1u;
-    for (int k = 0; k < G.num_objects; k++) {
+    const int nplace = full ? 24 : G.num_objects;
+    for (int k = 0; k < nplace; k++) {
         if (oc == 0) { G.err |= 8u; break; }
-        const int b = mask_choice(G, oc);
+        // full: `for objType in obj_types: for objColor in COLOR_NAMES` (no MT draw);
+        // else `choice(obj_choice); obj_choice.remove(...)`
+        const int b = full ? k : mask_choice(G, oc);
         if (G.abort) return 0;
         oc &= ~(1u << b);
         const int t = types[b / 6], cname = b % 6;
@@ -866,19 +892,138 @@ __device__ __forceinline__ int gen_single(Gen<NW> &G) {           // custom_env.
         add_obj(G, T_GOAL, 15, x, y);
     }
     place_agent(G);
+    if (full) cmd = pcg_integers(G.pcg, 0, 6);                     // np_random.choice(self.msn_commands)
     return cmd;
 }
 
 struct ResetOut {
     uint8_t tx, ty, ta, mission_id;
     int livelocks;
+    uint64_t range;        // 'move' target_range (move_range), 0 otherwise
 };
+
+// `obj_pos in [o[2] for o in objs]` (the objs list lives in LDS)
+template <int NW>
+__device__ __forceinline__ bool in_objs(const Gen<NW> &G, int x, int y) {
+    const uint32_t key = (uint32_t)x << 8 | (uint32_t)y << 16;
+    bool hit = false;
+    for (int k = 0; k < G.nobjs; k++) hit |= (G.objs[k] & 0xFFFF00u) == key;
+    return hit;
+}
+
+// Obstacles (custom_env.py:154-172), after the generator, before the mission target.
+//   multi:  while True: p=(randint(1,S-2), randint(1,S-2)); skip the middle row/column;
+//           skip p in objs; break if p != agent and not next2door(p)  -> put_obj(Lava())
+//   single: place_obj(choice([Lava(), Wall()]))
+template <int NW>
+__device__ __forceinline__ void place_obstacles(Gen<NW> &G) {
+    const int S = G.S, mid = S / 2;
+#pragma unroll 1
+    for (int k = 0; k < G.n_obstacles; k++) {
+        if (G.problem == 0) {
+            int x, y, rej = 0;
+            for (;;) {
+                x = randint(G, 1, S - 2);
+                y = randint(G, 1, S - 2);
+                if (G.abort) return;
+                const bool bad = x == mid || y == mid || in_objs(G, x, y) || (x == G.ax && y == G.ay) ||
+                                 next2door(G, x, y);
+                if (!bad) break;
+                if (++rej == SAT_PROBE) {            // provably unsatisfiable loop -> live-lock policy
+                    bool sat = false;
+                    for (int xx = 1; xx <= S - 2 && !sat; xx++)
+                        for (int yy = 1; yy <= S - 2 && !sat; yy++)
+                            sat = !(xx == mid || yy == mid || in_objs(G, xx, yy) || (xx == G.ax && yy == G.ay) ||
+                                    next2door(G, xx, yy));
+                    if (!sat) { live_lock(G); return; }
+                }
+            }
+            put(G, x, y, CODE_LAVA);
+        } else {
+            const bool lava = randbelow(G, 2) == 0;
+            if (G.abort) return;
+            int x, y;
+            draw_free_cell(G, x, y);
+            put(G, x, y, lava ? CODE_LAVA : CODE_WALL);
+        }
+    }
+}
+
+// 'move' target_range (custom_env.py:219-256): per row (left/right) or column (up/down)
+// k = 1..S-2, the first None cell scanning inward from that edge, if any.  Packed as
+// bits 0-1 = direction, bits 4k..4k+3 = that cell's x (rows) or y (columns), 0 = none.
+template <int NW>
+__device__ __forceinline__ uint64_t move_range(const Gen<NW> &G, int d) {
+    const int S = G.S;
+    uint64_t rg = (uint64_t)d;
+    for (int k = 1; k < S - 1; k++) {
+        int v;
+        bool ok;
+        if (d == 0) { v = 1; while (v < S - 1 && G.g[k * S + v] != CODE_EMPTY) v++; ok = v < S - 1; }
+        else if (d == 1) { v = S - 2; while (v > 0 && G.g[k * S + v] != CODE_EMPTY) v--; ok = v > 0; }
+        else if (d == 2) { v = 1; while (v < S - 1 && G.g[v * S + k] != CODE_EMPTY) v++; ok = v < S - 1; }
+        else { v = S - 2; while (v > 0 && G.g[v * S + k] != CODE_EMPTY) v--; ok = v > 0; }
+        if (ok) rg |= (uint64_t)v << (4 * k);
+    }
+    return rg;
+}
+// agent_pos in target_range
+__device__ __forceinline__ bool in_move_range(uint64_t rg, int ax, int ay) {
+    const bool rows = (rg & 3) < 2;
+    const int idx = rows ? ay : ax, coord = rows ? ax : ay;
+    const int ent = (int)((rg >> (4 * idx)) & 15);
+    return ent != 0 && ent == coord;
+}
+
+// Grid.process_vis(agent_pos=(3, 6)) + Grid.encode(vis_mask) (see_through_walls=False) on a
+// rendered frame (fr[c] type, fr[49+c] colour, fr[98+c] state, c = vx*7 + vy): cells the
+// agent cannot see become (0, 0, 0).  Bit-parallel over a view row (bit = vx): the
+// reference's left-to-right pass sets cell i+1 from a visible see-through cell i, i.e. the
+// closure of x |= (x & T) << 1; both passes also light cells i, i+1 (i-1, i) of the row
+// above.  The agent cell holds the carried object here, but the world cell under the
+// agent is always see-through (it can overlap it), as is any carried object.
+__device__ __forceinline__ void apply_vis(uint8_t *fr) {
+    uint32_t T[7];
+#pragma unroll
+    for (int vy = 0; vy < 7; vy++) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int vx = 0; vx < 7; vx++) {
+            const int c = vx * 7 + vy;
+            const int ty = fr[c], st = fr[98 + c];
+            const bool opaque = ty == T_WALL || (ty == T_DOOR && st != 0);   // see_behind() false
+            t |= (uint32_t)!opaque << vx;
+        }
+        T[vy] = t;
+    }
+    uint64_t vis = 0;
+    uint32_t m = 1u << 3;                    // mask[3][6] = True
+#pragma unroll
+    for (int j = 6; j >= 0; j--) {
+        const uint32_t t = T[j];
+        uint32_t x = m;
+#pragma unroll
+        for (int k = 0; k < 6; k++) x |= (x & t & 0x3Fu) << 1;     // for i in range(0, 6)
+        const uint32_t s1 = x & t & 0x3Fu;
+        uint32_t up = (s1 << 1) | s1;
+#pragma unroll
+        for (int k = 0; k < 6; k++) x |= (x & t & 0x7Eu) >> 1;     // for i in reversed(range(1, 7))
+        const uint32_t s2 = x & t & 0x7Eu;
+        up |= (s2 >> 1) | s2;
+#pragma unroll
+        for (int vx = 0; vx < 7; vx++) vis |= (uint64_t)((x >> vx) & 1u) << (vx * 7 + j);
+        m = up;
+    }
+#pragma unroll
+    for (int c = 0; c < 49; c++)
+        if (!((vis >> c) & 1ull)) { fr[c] = 0; fr[49 + c] = 0; fr[98 + c] = 0; }
+}
 
 template <int NW>
 __device__ __forceinline__ void gen_init(Gen<NW> &G) {}
 
 // One attempt of MiniGridEnv.reset -> PlaygroundEnv._gen_grid (custom_env.py:122-267).
-template <int NW>
+template <int NW, bool EXT>
 __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
     const int S = G.S;
     {   // Grid(W, H) of None + wall_rect(0, 0, W, H); the row is 4-B aligned in LDS
@@ -898,9 +1043,20 @@ __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
     G.dn.clear();
     G.ax = -1; G.ay = -1; G.adir = 0; G.nobjs = 0; G.tmask = 0;
     GSTAMP(G, 9);                                                 // attempt setup (mt_sync, grid clear)
-    const int cmd = G.problem == 0 ? gen_multi(G) : gen_single(G);
+    const int cmd = G.problem == 0 ? gen_multi(G) : gen_single<NW, EXT>(G);
     if (G.abort) return;
-    if (cmd == 0) {                                               // 'go to' (np_random.integers)
+    if (EXT && G.n_obstacles) {
+        place_obstacles(G);
+        if (G.abort) return;
+    }
+    R.range = 0;
+    if (EXT && cmd == 3) {                                        // 'drop'
+        R.tx = R.ty = NONE8; R.ta = A_DROP; R.mission_id = MID_DROP;
+    } else if (EXT && cmd == 4) {                                 // 'move <dir>'
+        const int d = pcg_integers(G.pcg, 0, 4);                  // np_random.choice(self.msn_directions)
+        R.range = move_range(G, d);
+        R.tx = R.ty = NONE8; R.ta = NONE8; R.mission_id = (uint8_t)(MID_MOVE + d);
+    } else if (cmd == 0) {                                               // 'go to' (np_random.integers)
         int i = 0;
         for (uint32_t it = 0;; ++it) {
             if (it > PCG_LOOP_LIMIT) { G.err |= 4u; break; }
@@ -934,7 +1090,7 @@ __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
 }
 
 // MiniGridEnv.reset with the engine's live-lock retry policy.
-template <int NW>
+template <int NW, bool EXT>
 __device__ __forceinline__ void reset_env(Gen<NW> &G, ResetOut &R) {
     R.livelocks = 0;
     for (;;) {
@@ -942,7 +1098,7 @@ __device__ __forceinline__ void reset_env(Gen<NW> &G, ResetOut &R) {
         G.astart = G.cur;
         G.abort = false;
         mt_sync(G);                     // register queue at the attempt's first word
-        gen_attempt(G, R);
+        gen_attempt<NW, EXT>(G, R);
         GSTAMP(G, 15);                  // mission target selection
         if (!G.abort) break;
         R.livelocks++;

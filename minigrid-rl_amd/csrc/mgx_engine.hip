@@ -58,6 +58,11 @@ struct KParams {
     int S, GS, GSL, grid_lds, n_stack, img_bytes, stk_lds, stk_step, problem, cfg_mission, num_objects, all_doors_open;
     uint32_t llw;
     int terminal_mode, mission64, fast_roll;
+    int n_obstacles;        // floor((S-2)^2 * percent_obstacles) when cfg.obstacles (custom_env.py:156)
+    int vis;                // see_through_walls == False: Grid.process_vis on every frame
+    int has_move;           // the problem can draw 'move' missions: target_range words below are live
+    uint64_t *range_cur;    // [N]     target_range of the current episode (mgx_device.h: move_range)
+    uint64_t *ring_range;   // [N][D]  ... of each queued episode
     // pre-generated episode ring (see mgx_refill_kernel)
     uint8_t *ring_grid;     // [N][D][GS]
     uint4 *ring_hdr;        // [N][D][3] {ax|ay<<8|dir<<16|tx<<24, ty|ta<<8|mission<<16, livelocks, 0},
@@ -241,6 +246,7 @@ __device__ __forceinline__ void load_gen(Gen<NW> &G, const KParams &p, int64_t e
     G.cfg_mission = p.cfg_mission;
     G.num_objects = p.num_objects;
     G.all_doors_open = p.all_doors_open;
+    G.n_obstacles = p.n_obstacles;
     G.abort = false;
     G.nobjs = 0;
     G.ax = G.ay = -1;
@@ -292,10 +298,11 @@ __device__ __forceinline__ void write_fresh_frame(const KParams &p, uint8_t *img
         dst[49 + k] = (uint8_t)(v >> 8);
         dst[98 + k] = (uint8_t)(v >> 16);
     });
+    if (p.vis) apply_vis(dst);          // this thread's own global writes: read back coherently
 }
 
 // ============================================================== reset kernel
-template <int NW>
+template <int NW, bool EXT>
 __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOut o) {
     extern __shared__ __align__(16) uint8_t smem[];
     uint8_t *s_scr = smem;
@@ -337,12 +344,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
         }
         G.gbase = ~0ull >> 1;
         ResetOut R;
-        reset_env(G, R);
+        reset_env<NW, EXT>(G, R);
         st.ax = (uint8_t)G.ax; st.ay = (uint8_t)G.ay; st.dir = (uint8_t)G.adir; st.carry = 0;
         st.step_count = 0;
         st.tx = R.tx; st.ty = R.ty; st.target_action = R.ta; st.mission_id = R.mission_id;
         st.frames = 1; st.flags = 0; st.pad = 0;
         p.state[e] = st;
+        if (p.has_move) p.range_cur[e] = R.range;
         store_rng(G, p, e);
         rng_snapshot(G, p.cur_rng + 2 * e);
         p.ring_head[e] = 0; p.ring_tail[e] = 0; p.ring_pub[e] = 0;   // empty ring (mgx_refill_kernel fills)
@@ -465,8 +473,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     int a = 0;
     uint4 odir = make_uint4(0, 0, 0, 0);          // old direction stack (n_stack == 4: one uint4)
     uint8_t rhead = 0, rpub = 0;                  // this env's ring position and published end
+    uint64_t mrange = 0;                          // 'move' target_range (problems mov / full only)
     if (tid < ne) {
         st = p.state[e0 + tid];
+        if (p.has_move) mrange = p.range_cur[e0 + tid];
         a = (int)actions[e0 + tid];
         if (p.n_stack == 4) odir = reinterpret_cast<const uint4 *>(o.dir)[e0 + tid];
         if (p.D > 0) { rhead = p.ring_head[e0 + tid]; rpub = p.ring_pub[e0 + tid]; }
@@ -660,6 +670,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
                 }
                 if (arrived && a == (int)st.target_action) { if (rs < 0) rs = sc; mdone = 1; }
                 if (!has_t && st.target_action != NONE8 && a == (int)st.target_action) { if (rs < 0) rs = sc; mdone = 1; }
+                if (st.mission_id >= MID_MOVE && in_move_range(mrange, ax, ay)) { if (rs < 0) rs = sc; mdone = 1; }
             }
             if (a == A_DONE) {
                 rew = mdone ? reward_at(rs, ms) : 0.0;    // stored self.reward, or 0 (not manual)
@@ -683,6 +694,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         const bool avail = done && p.D > 0 && (uint8_t)(rpub - rhead) != 0;
         const bool filling = !done && st.frames < p.n_stack;
         uint4 rng0 = make_uint4(0, 0, 0, 0), rng1 = rng0;
+        uint64_t nrange = 0;
         if (avail) {
             const int64_t slot = e * p.D + (rhead & (p.D - 1));
             __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot, s_phdr, 16, 0, 0);
@@ -693,6 +705,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
                 __builtin_amdgcn_global_load_lds(gsrc + c, s_pgrid + c * (BLOCK_ENVS * 16), 16, 0, 0);
             rng0 = p.ring_rng[2 * slot];
             rng1 = p.ring_rng[2 * slot + 1];
+            if (p.has_move) nrange = p.ring_range[slot];
         } else if (filling) {                               // tokens of the mission that stays
             const uint4 *t = reinterpret_cast<const uint4 *>(p.mtok + st.mission_id * 32);
             __builtin_amdgcn_global_load_lds(t, s_tokA, 16, 0, 0);
@@ -703,6 +716,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             const uint4 h = s_phdr[tid];
             p.cur_rng[2 * e] = rng0;
             p.cur_rng[2 * e + 1] = rng1;
+            if (p.has_move) p.range_cur[e] = nrange;
             new_head = (int)(uint8_t)(rhead + 1);   // published after a barrier, loads consumed
             const int nax = h.x & 0xFF, nay = (h.x >> 8) & 0xFF, ndir = (h.x >> 16) & 0xFF;
             const uint8_t mid = (uint8_t)(h.y >> 16);
@@ -773,6 +787,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // ---- phase 2b: render every env's frame (all 256 threads)
     render_block(s_grid, s_stk, s_rp, nullptr, ne, S, p.GSL, FSTRIDE, FOFF);
     __syncthreads();
+    if (p.vis) {                                       // see_through_walls=False: process_vis
+        if (tid < ne) apply_vis(s_stk + tid * FSTRIDE + FOFF);
+        __syncthreads();
+    }
 #ifdef MGX_STAMPS
     tsB = __builtin_amdgcn_s_memtime();
 #endif
@@ -802,6 +820,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         __syncthreads();
         // first frames of the new episodes -> frame rows (phase 3 zero-fills the older slots)
         render_block(s_grid, s_stk, s_rp2, s_dlist, s_npop, S, p.GSL, FSTRIDE, FOFF);
+        if (p.vis) {
+            __syncthreads();
+            if (tid < s_npop) apply_vis(s_stk + s_dlist[tid] * FSTRIDE + FOFF);
+        }
     }
     __syncthreads();
     // mission stacks, block-cooperative and coalesced: fresh stacks of popped envs
@@ -958,7 +980,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
 // empty ring (normally none; every done env when the ring is disabled), and writes
 // that env's reset outputs.  Grid-stride over the list; the last workgroup to
 // finish clears the list for the next step.
-template <int NW>
+template <int NW, bool EXT>
 __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int tid = threadIdx.x;
@@ -973,7 +995,7 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
         load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
         load_rng(G, p, e);
         ResetOut R;
-        reset_env(G, R);
+        reset_env<NW, EXT>(G, R);
         store_rng(G, p, e);
         rng_snapshot(G, p.cur_rng + 2 * e);
         {
@@ -989,6 +1011,7 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
         ns.tx = R.tx; ns.ty = R.ty; ns.target_action = R.ta; ns.mission_id = R.mission_id;
         ns.frames = 1; ns.flags = 0; ns.pad = 0;
         p.state[e] = ns;
+        if (p.has_move) p.range_cur[e] = R.range;
         write_fresh_frame(p, o.img, e, G.g, G.ax, G.ay, G.adir);   // older slots were zeroed by the step
         dir_stack_fresh(o.dir, e, p.n_stack, G.adir);
         write_mission_stack(o.mis, p.mission64, e, p.n_stack, 1, p.mtok + R.mission_id * 32);
@@ -1023,7 +1046,7 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
 // off the step kernel's critical path.  Episodes are generated in exactly the
 // order the env will consume them, so RNG streams advance as in the reference.
 // One wave per workgroup; all LDS is lane-private (grid row + MT window + objs).
-template <int NW>
+template <int NW, bool EXT>
 __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int tid = threadIdx.x;
@@ -1058,7 +1081,7 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
                 G.astart = G.cur;
                 G.abort = false;
                 mt_sync(G);
-                gen_attempt(G, R);
+                gen_attempt<NW, EXT>(G, R);
                 if (G.abort && ++livelocks <= 100000) continue;
                 if (G.abort) G.err |= 4u;           // give up on this env (reported, never silent)
                 R.livelocks = livelocks;
@@ -1074,6 +1097,7 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
                 p.ring_hdr[3 * slot + 1] = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[0];
                 p.ring_hdr[3 * slot + 2] = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[1];
                 rng_snapshot(G, p.ring_rng + 2 * slot);
+                if (EXT && p.has_move) p.ring_range[slot] = R.range;
                 tail++;
             }
             store_rng(G, p, e);
@@ -1234,8 +1258,13 @@ const char *CMD_TXT[3] = {"go to", "toggle", "pick up"};
 const char *CN_TXT[6] = {"blue", "green", "grey", "purple", "red", "yellow"};
 const char *TS_TXT[4] = {"door", "key", "ball", "box"};
 
+const char *DIR_TXT[4] = {"left", "right", "up", "down"};
+
 bool mission_text(int id, std::string &out) {
     if (id < 0 || id > 255) return false;
+    if (id == MID_DROP) { out = "drop"; return true; }
+    if (id >= MID_MOVE && id < MID_MOVE + 4) { out = std::string("move ") + DIR_TXT[id - MID_MOVE]; return true; }
+    if (id >= 128) return false;
     int cmd = id & 3, cn = (id >> 2) & 7, ts = (id >> 5) & 3;
     if (cmd == CMD_GOTOGOAL) { out = "go to goal"; return id == CMD_GOTOGOAL; }
     if (cn > 5) return false;
@@ -1251,6 +1280,7 @@ struct mgx_handle {
     KParams kp;
     size_t lds_step, lds_reset, lds_refill;
     int nw;                 // 64-bit words of the generator's S*S cell masks (1, 2 or 4)
+    bool ext;               // generator variant with full / drp / mov / obstacles
     int refill_every;       // K: steps per refill epoch
     uint64_t calls;         // mgx_step calls since the last mgx_reset
     uint64_t resets;        // mgx_reset calls since create
@@ -1275,13 +1305,21 @@ mgx_status mgx_mission_text(int mission_id, char *buf, size_t buflen) {
     return MGX_OK;
 }
 
+// range(floor((size - 2)**2 * percent_obstacles)) (custom_env.py:156), fp64 like Python
+static int n_obstacles_of(const mgx_config *c) {
+    if (!c->obstacles) return 0;
+    return (int)std::floor((double)((c->size - 2) * (c->size - 2)) * c->percent_obstacles);
+}
+
 static mgx_status validate(const mgx_config *c) {
     if (!c) return fail(MGX_ERR_INVALID, "null config");
     if (c->size < 5 || c->size > 16) return fail(MGX_ERR_INVALID, "size must be in 5..16");
     if (c->n_envs <= 0) return fail(MGX_ERR_INVALID, "n_envs must be > 0");
     if (c->n_stack < 1 || c->n_stack > 8) return fail(MGX_ERR_INVALID, "n_stack must be in 1..8");
-    if (!c->see_through_walls) return fail(MGX_ERR_INVALID, "see_through_walls=false (process_vis) is not supported");
-    if (c->obstacles) return fail(MGX_ERR_INVALID, "obstacles=true is not supported");
+    if (c->obstacles && !(c->percent_obstacles >= 0.0 && c->percent_obstacles <= 1.0))
+        return fail(MGX_ERR_INVALID, "percent_obstacles must be in [0, 1]");
+    const int interior = (c->size - 2) * (c->size - 2);
+    const int nobst = n_obstacles_of(c);
     switch (c->problem) {
         case MGX_PROBLEM_MULTI:
             if (!(c->mission == -1 || c->mission == 0 || c->mission == 1 || c->mission == 2 || c->mission == 5))
@@ -1297,12 +1335,24 @@ static mgx_status validate(const mgx_config *c) {
         case MGX_PROBLEM_PKP:
             if (c->num_objects > 18) return fail(MGX_ERR_INVALID, "Number of objects to be generated is more than the available objects.");
             break;
-        case MGX_PROBLEM_FULL: case MGX_PROBLEM_DRP: case MGX_PROBLEM_MOV:
-            return fail(MGX_ERR_INVALID, "problem full/drp/mov is not built yet (DESIGN.md, next)");
+        case MGX_PROBLEM_DRP: case MGX_PROBLEM_MOV:
+            if (c->num_objects > 24) return fail(MGX_ERR_INVALID, "Number of objects to be generated is more than the available objects.");
+            break;
+        case MGX_PROBLEM_FULL:
+            break;
         default:
             return fail(MGX_ERR_INVALID, "Invalid problem type given");
     }
     if (c->num_objects < 0) return fail(MGX_ERR_INVALID, "num_objects must be >= 0");
+    if (c->problem != MGX_PROBLEM_MULTI) {
+        // single room: every object, [goal], the agent and each obstacle take one free interior
+        // cell via place_obj, which never gives up (max_tries=inf): more than fit = a hang
+        const bool goal = c->problem == MGX_PROBLEM_GTG || c->problem == MGX_PROBLEM_DRP || c->problem == MGX_PROBLEM_FULL;
+        const int cells = (c->problem == MGX_PROBLEM_FULL ? 24 : c->num_objects) + (goal ? 1 : 0) + 1 + nobst;
+        if (cells > interior)
+            return fail(MGX_ERR_INVALID, "the room cannot hold the objects, goal, agent and obstacles "
+                                         "(the reference's place_obj would never return)");
+    }
     if (c->terminal_mode < 0 || c->terminal_mode > 2) return fail(MGX_ERR_INVALID, "bad terminal_mode");
     return MGX_OK;
 }
@@ -1431,6 +1481,9 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.all_doors_open = cfg->all_doors_open;
     p.llw = (uint32_t)h->cfg.livelock_words;
     p.terminal_mode = cfg->terminal_mode;
+    p.n_obstacles = n_obstacles_of(cfg);
+    p.vis = cfg->see_through_walls ? 0 : 1;
+    p.has_move = (cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL) ? 1 : 0;
     p.ring_grid = (uint8_t *)h->allocs[7];
     p.ring_hdr = (uint4 *)h->allocs[8];
     p.ring_rng = (uint4 *)h->allocs[9];
@@ -1449,6 +1502,16 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset stats"));
         p.blk = (ulonglong4 *)h->allocs[13];
     }
+    {   // 'move' target_range words: current episode [N] + ring [N][D] (16 B when unused)
+        const bool mv = cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL;
+        const size_t bytes = mv ? (size_t)N * (1 + (size_t)D) * 8 : 16;
+        hipError_t e = hipMalloc(&h->allocs[14], bytes);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc move ranges"));
+        e = hipMemset(h->allocs[14], 0, bytes);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset move ranges"));
+        p.range_cur = (uint64_t *)h->allocs[14];
+        p.ring_range = mv ? p.range_cur + N : p.range_cur;
+    }
     p.D = D;
     p.K = h->cfg.refill_every;
     p.cap = h->cfg.refill_cap;
@@ -1459,15 +1522,19 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
-#define MGX_SET_LDS(K, bytes)                                                                            \
-    HIP_TRY(hipFuncSetAttribute((const void *)K<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes))); \
-    HIP_TRY(hipFuncSetAttribute((const void *)K<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes))); \
-    HIP_TRY(hipFuncSetAttribute((const void *)K<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes)))
+    h->ext = cfg->obstacles || cfg->problem == MGX_PROBLEM_FULL || cfg->problem == MGX_PROBLEM_DRP ||
+             cfg->problem == MGX_PROBLEM_MOV;
+#define MGX_SET_LDS1(K, bytes) \
+    HIP_TRY(hipFuncSetAttribute((const void *)K, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes)))
+#define MGX_SET_LDS(K, bytes)                                                                  \
+    MGX_SET_LDS1((K<1, false>), bytes); MGX_SET_LDS1((K<2, false>), bytes); MGX_SET_LDS1((K<4, false>), bytes); \
+    MGX_SET_LDS1((K<1, true>), bytes); MGX_SET_LDS1((K<2, true>), bytes); MGX_SET_LDS1((K<4, true>), bytes)
     MGX_SET_LDS(mgx_reset_kernel, h->lds_reset);
     h->lds_refill = (size_t)((64 * (GS + 4) + 15) & ~15) + (size_t)64 * SCRATCH_PER_ENV;
     MGX_SET_LDS(mgx_refill_kernel, h->lds_refill);
     MGX_SET_LDS(mgx_fixup_kernel, h->lds_refill);
 #undef MGX_SET_LDS
+#undef MGX_SET_LDS1
     {
         hipError_t e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
@@ -1496,14 +1563,22 @@ mgx_status mgx_destroy(mgx_handle *h) {
     return MGX_OK;
 }
 
+// Launch generator kernel K<NW, EXT> for this handle's mask width and feature variant.
+#define MGX_GEN_LAUNCH(K, ...)                                                                    \
+    do {                                                                                          \
+        const int v_ = h->nw | (h->ext ? 8 : 0);                                                  \
+        if (v_ == 1) hipLaunchKernelGGL((K<1, false>), __VA_ARGS__);                              \
+        else if (v_ == 2) hipLaunchKernelGGL((K<2, false>), __VA_ARGS__);                         \
+        else if (v_ == 4) hipLaunchKernelGGL((K<4, false>), __VA_ARGS__);                         \
+        else if (v_ == 9) hipLaunchKernelGGL((K<1, true>), __VA_ARGS__);                          \
+        else if (v_ == 10) hipLaunchKernelGGL((K<2, true>), __VA_ARGS__);                         \
+        else hipLaunchKernelGGL((K<4, true>), __VA_ARGS__);                                       \
+    } while (0)
+
 static mgx_status launch_refill(mgx_handle *h, void *stream) {
     if (h->kp.D == 0) return MGX_OK;
     const int64_t nblk = (h->kp.n + 63) / 64;
-    switch (h->nw) {
-        case 1: hipLaunchKernelGGL(mgx_refill_kernel<1>, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp); break;
-        case 2: hipLaunchKernelGGL(mgx_refill_kernel<2>, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp); break;
-        default: hipLaunchKernelGGL(mgx_refill_kernel<4>, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp); break;
-    }
+    MGX_GEN_LAUNCH(mgx_refill_kernel, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp);
     HIP_TRY(hipGetLastError());
     return MGX_OK;
 }
@@ -1568,11 +1643,7 @@ mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, v
     h->kp.reset_mode = h->resets == 0 ? 0 : (h->seed_pending ? 1 : 2);
     h->resets++;
     h->seed_pending = false;
-    switch (h->nw) {
-        case 1: hipLaunchKernelGGL(mgx_reset_kernel<1>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
-        case 2: hipLaunchKernelGGL(mgx_reset_kernel<2>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
-        default: hipLaunchKernelGGL(mgx_reset_kernel<4>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o); break;
-    }
+    MGX_GEN_LAUNCH(mgx_reset_kernel, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o);
     HIP_TRY(hipGetLastError());
     h->calls = 0;
     h->kp.initial_fill = 1;                     // fills every ring to 2K (synchronously on `stream`)
@@ -1631,11 +1702,7 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
     HIP_TRY(hipGetLastError());
     if (h->kp.D == 0) {   // no ring: every done env is generated inline, right after the step
         const unsigned fblk = (unsigned)h->kp.nblk;
-        switch (h->nw) {
-            case 1: hipLaunchKernelGGL(mgx_fixup_kernel<1>, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o); break;
-            case 2: hipLaunchKernelGGL(mgx_fixup_kernel<2>, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o); break;
-            default: hipLaunchKernelGGL(mgx_fixup_kernel<4>, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o); break;
-        }
+        MGX_GEN_LAUNCH(mgx_fixup_kernel, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o);
         HIP_TRY(hipGetLastError());
     }
     h->calls++;

@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MGX_LIB_PATH", os.path.join(HERE, "libmgx.so"))   # override: diagnostic builds
 
 MGX_OK = 0
+ABI_VERSION = 2        # == MGX_ABI_VERSION (include/mgx.h)
 PROBLEMS = {"multi": 0, "full": 1, "gto": 2, "gtg": 3, "opn": 4, "pkp": 5, "drp": 6, "mov": 7}
 TERMINAL = {"none": 0, "truncated": 1, "all": 2}
 DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unknown action)",
@@ -34,6 +35,7 @@ class MgxConfig(ctypes.Structure):
         ("livelock_words", ctypes.c_int32), ("terminal_mode", ctypes.c_int32),
         ("mission_int64", ctypes.c_int32), ("refill_cap", ctypes.c_int32), ("mt_table_words", ctypes.c_int64),
         ("ring_depth", ctypes.c_int32), ("refill_every", ctypes.c_int32),
+        ("percent_obstacles", ctypes.c_double),
     ]
 
 
@@ -85,7 +87,7 @@ def load():
     L.mgx_mission_text.argtypes = [I, ctypes.c_char_p, ctypes.c_size_t]
     for name in EXPORTS:
         getattr(L, name).restype = getattr(L, name).restype or I
-    if L.mgx_abi_version() != 1:
+    if L.mgx_abi_version() != ABI_VERSION:
         raise MgxError("libmgx ABI mismatch")
     _lib = L
     return L

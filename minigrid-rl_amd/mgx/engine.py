@@ -23,7 +23,7 @@ def _ptr(t):
 class MgxEngine:
     def __init__(self, problem="multi", mission=5, size=8, num_objects=4, n_envs=65536, seed=42,
                  env_index_offset=0, n_stack=4, all_doors_open=False, see_through_walls=True,
-                 obstacles=False, terminal_mode="truncated", mission_dtype=torch.int64,
+                 obstacles=False, percent_obstacles=0.05, terminal_mode="truncated", mission_dtype=torch.int64,
                  device="cuda", livelock_words=0, mt_table_words=0, reward64=False, ring_depth=0,
                  refill_every=0, refill_cap=0):
         self.L = _lib.load()
@@ -47,6 +47,7 @@ class MgxEngine:
         cfg.see_through_walls = int(bool(see_through_walls))
         cfg.all_doors_open = int(bool(all_doors_open))
         cfg.obstacles = int(bool(obstacles))
+        cfg.percent_obstacles = float(percent_obstacles)
         cfg.n_stack = self.n_stack
         cfg.n_envs = self.n
         cfg.base_seed = self.seed

@@ -8,7 +8,11 @@
  * What it restates, function by function (file:line into /root/reference):
  *   PlaygroundEnv._gen_grid            src/custom_env.py:122-267
  *   PlaygroundEnv.step                 src/custom_env.py:269-330
+ *   obstacles (cfg.obstacles)          src/custom_env.py:154-172
+ *   'move' target_range                src/custom_env.py:219-256
+ *   _generate_full_map                 src/custom_env.py:332-369
  *   _generate_{gto,gtg,open,pkp}_map   src/custom_env.py:371-513
+ *   _generate_{drop,move}_map          src/custom_env.py:515-593
  *   _generate_multi_map                src/custom_env.py:595-615
  *   _generate_2_rooms                  src/custom_env.py:617-855
  *   _generate_3_rooms                  src/custom_env.py:857-1297
@@ -18,8 +22,8 @@
  *   Discrete2BoxWrapper                src/environment.py:138-149
  * and the third-party semantics they call (not vendored; SURVEY.md App. A,
  * parity unpinned at that boundary): minigrid MiniGridEnv.{reset,step,
- * gen_obs,place_obj,place_agent,put_obj,_reward}, Grid.{slice,rotate_left,
- * encode}, world objects; CPython random (MT19937 init_by_array,
+ * gen_obs,gen_obs_grid,place_obj,place_agent,put_obj,_reward},
+ * Grid.{slice,rotate_left,encode,process_vis}, world objects (see_behind); CPython random (MT19937 init_by_array,
  * getrandbits, _randbelow, choice, randint); numpy SeedSequence + PCG64 +
  * Generator.integers (Lemire32 over the has_uint32-buffered next_uint32);
  * SB3 SubprocVecEnv auto-reset (each env owns an MT19937 seeded cfg.seed).
@@ -242,6 +246,7 @@ static const char *CMD_NAME[6] = {"go to", "toggle", "pick up", "drop", "move", 
 
 typedef struct {
     int S, max_steps, problem, cfg_mission, num_objects, all_doors_open;
+    int see_through_walls, n_obstacles;
     cell_t grid[MAXS * MAXS];
     int ax, ay, adir;
     cell_t carrying; /* type O_NONE == None */
@@ -256,6 +261,7 @@ typedef struct {
     pcg_t pcg;
     jmp_buf jb;
     objrec_t objs[MAXOBJ]; int nobjs;
+    int range_x[MAXS * 2], range_y[MAXS * 2], nrange;   /* self.target_range */
 } env_t;
 
 typedef struct {
@@ -286,6 +292,7 @@ static cell_t mk(int type, int color) { cell_t c = {(uint8_t)type, (uint8_t)colo
 static cell_t mk_none(void) { return mk(O_NONE, 0); }
 static cell_t mk_wall(void) { return mk(O_WALL, C_GREY); }
 static cell_t mk_goal(void) { return mk(O_GOAL, C_GREEN); }
+static cell_t mk_lava(void) { return mk(O_LAVA, C_RED); }
 static cell_t mk_door(int cname, int locked, int open) {
     cell_t c = mk(O_DOOR, CN2IDX[cname]); c.is_locked = (uint8_t)locked; c.is_open = (uint8_t)open; return c;
 }
@@ -300,6 +307,7 @@ static void encode_cell(const cell_t *c, uint8_t out[3]) {
 static int can_overlap(const cell_t *c) {
     return c->type == O_GOAL || c->type == O_LAVA || (c->type == O_DOOR && c->is_open);
 }
+static int see_behind(const cell_t *c) { return c->type == O_WALL ? 0 : (c->type == O_DOOR ? c->is_open : 1); }
 static int can_pickup(const cell_t *c) { return c->type == O_KEY || c->type == O_BALL || c->type == O_BOX; }
 
 static int next2door(env_t *e, int x, int y) {
@@ -613,11 +621,26 @@ static int gen_single(env_t *e) {
     static const int PKP_T[3] = {O_KEY, O_BOX, O_BALL};
     olist_t oc;
     int goal = 0, cmd;
+    if (e->problem == P_FULL) {                 /* _generate_full_map (custom_env.py:332-369) */
+        for (int t = 0; t < 4; t++)             /* for objType in obj_types: for objColor in COLOR_NAMES */
+            for (int c = 0; c < 6; c++) {
+                int x, y;
+                place_obj(e, mk(GTO_T[t], CN2IDX[c]), &x, &y);
+                add_obj(e, GTO_T[t], c, x, y);
+            }
+        int x, y;
+        place_obj(e, mk_goal(), &x, &y);
+        add_obj(e, O_GOAL, -1, x, y);
+        place_agent(e);
+        return rint_np(e, 0, 6);                /* np_random.choice(self.msn_commands) */
+    }
     switch (e->problem) {
         case P_GTO: ol_init(&oc, GTO_T, 4); cmd = CMD_GOTO; break;
         case P_GTG: ol_init(&oc, GTG_T, 4); cmd = CMD_GOTOGOAL; goal = 1; break;
         case P_OPN: ol_init(&oc, OPN_T, 2); cmd = CMD_TOGGLE; break;
         case P_PKP: ol_init(&oc, PKP_T, 3); cmd = CMD_PICKUP; break;
+        case P_DRP: ol_init(&oc, GTO_T, 4); cmd = CMD_DROP; goal = 1; break;   /* custom_env.py:515-554 */
+        case P_MOV: ol_init(&oc, GTO_T, 4); cmd = CMD_MOVE; break;             /* custom_env.py:556-593 */
         default: fprintf(stderr, "oracle: unsupported problem %d\n", e->problem); abort();
     }
     if (oc.n < e->num_objects) { fprintf(stderr, "oracle: too many objects\n"); abort(); }
@@ -651,7 +674,26 @@ static void gen_grid(env_t *e) {               /* custom_env.py:122-267 */
     e->target_action = -1; e->has_tpos = 0; e->mission[0] = 0; e->nobjs = 0;
     for (int i = 0; i < S; i++) { gset(e, i, 0, mk_wall()); gset(e, i, S - 1, mk_wall()); }
     for (int j = 0; j < S; j++) { gset(e, 0, j, mk_wall()); gset(e, S - 1, j, mk_wall()); }
+    e->nrange = 0;
     int cmd = e->problem == P_MULTI ? gen_multi(e) : gen_single(e);
+    /* obstacles (custom_env.py:154-172) */
+    for (int k = 0; k < e->n_obstacles; k++) {
+        if (e->problem == P_MULTI) {
+            int mid = S / 2, x, y;
+            for (;;) {
+                x = randint(e, 1, S - 2);
+                y = randint(e, 1, S - 2);
+                if (x == mid || y == mid) continue;
+                if (in_objs(e, x, y)) continue;
+                if (!(x == e->ax && y == e->ay) && !next2door(e, x, y)) break;
+            }
+            gset(e, x, y, mk_lava());                       /* put_obj(Lava(), ...) */
+        } else {
+            int lava = randbelow(e, 2) == 0;                /* choice([Lava(), Wall()]) */
+            int x, y;
+            place_obj(e, lava ? mk_lava() : mk_wall(), &x, &y);
+        }
+    }
     switch (cmd) {
         case CMD_GOTO: {
             int i;
@@ -679,6 +721,29 @@ static void gen_grid(env_t *e) {               /* custom_env.py:122-267 */
             for (int i = 0; i < e->nobjs; i++)
                 if (e->objs[i].type == O_GOAL) { e->has_tpos = 1; e->tx = e->objs[i].x; e->ty = e->objs[i].y; found = 1; break; }
             if (!found) { fprintf(stderr, "oracle: Invalid mission generated\n"); abort(); }
+            break;
+        }
+        case CMD_DROP:
+            snprintf(e->mission, sizeof e->mission, "drop");
+            e->target_action = A_DROP;
+            break;
+        case CMD_MOVE: {
+            static const char *DIRS[4] = {"left", "right", "up", "down"};
+            int d = rint_np(e, 0, 4);                       /* np_random.choice(self.msn_directions) */
+            for (int k = 1; k < S - 1; k++) {
+                int x, y;
+                switch (d) {
+                    case 0: y = k; x = 1; while (x < S - 1 && G(e, x, y)->type != O_NONE) x++;
+                        if (x < S - 1) { e->range_x[e->nrange] = x; e->range_y[e->nrange++] = y; } break;
+                    case 1: y = k; x = S - 2; while (x > 0 && G(e, x, y)->type != O_NONE) x--;
+                        if (x > 0) { e->range_x[e->nrange] = x; e->range_y[e->nrange++] = y; } break;
+                    case 2: x = k; y = 1; while (y < S - 1 && G(e, x, y)->type != O_NONE) y++;
+                        if (y < S - 1) { e->range_x[e->nrange] = x; e->range_y[e->nrange++] = y; } break;
+                    default: x = k; y = S - 2; while (y > 0 && G(e, x, y)->type != O_NONE) y--;
+                        if (y > 0) { e->range_x[e->nrange] = x; e->range_y[e->nrange++] = y; } break;
+                }
+            }
+            snprintf(e->mission, sizeof e->mission, "move %s", DIRS[d]);
             break;
         }
         default: fprintf(stderr, "oracle: unsupported mission command %d\n", cmd); abort();
@@ -724,8 +789,31 @@ static void gen_obs(env_t *e, uint8_t img[7][7][3]) {
         for (int i = 0; i < 7; i++) for (int j = 0; j < 7; j++) b[j][6 - i] = a[i][j];
         memcpy(a, b, sizeof a);
     }
+    int vis[7][7];
+    for (int i = 0; i < 7; i++) for (int j = 0; j < 7; j++) vis[i][j] = e->see_through_walls;
+    if (!e->see_through_walls) {                /* Grid.process_vis(agent_pos=(3, 6)) */
+        vis[3][6] = 1;
+        for (int j = 6; j >= 0; j--) {
+            for (int i = 0; i < 6; i++) {
+                if (!vis[i][j]) continue;
+                if (a[i][j].type != O_NONE && !see_behind(&a[i][j])) continue;
+                vis[i + 1][j] = 1;
+                if (j > 0) { vis[i + 1][j - 1] = 1; vis[i][j - 1] = 1; }
+            }
+            for (int i = 6; i >= 1; i--) {
+                if (!vis[i][j]) continue;
+                if (a[i][j].type != O_NONE && !see_behind(&a[i][j])) continue;
+                vis[i - 1][j] = 1;
+                if (j > 0) { vis[i - 1][j - 1] = 1; vis[i][j - 1] = 1; }
+            }
+        }
+    }
     a[3][6] = e->carrying;                      /* carrying or None */
-    for (int i = 0; i < 7; i++) for (int j = 0; j < 7; j++) encode_cell(&a[i][j], img[i][j]);
+    for (int i = 0; i < 7; i++)
+        for (int j = 0; j < 7; j++) {
+            if (vis[i][j]) encode_cell(&a[i][j], img[i][j]);
+            else img[i][j][0] = img[i][j][1] = img[i][j][2] = 0;   /* encode(vis_mask): unseen */
+        }
 }
 
 static void tokenize(const char *m, uint8_t out[32]) {   /* environment.py:91-105 */
@@ -818,7 +906,12 @@ static void env_step(env_t *e, int action, uint8_t img[7][7][3], double *rew, in
             if (!e->has_reward) { e->reward = env_reward_at(e); e->has_reward = 1; }
             e->mission_done = 1;
         }
-        /* target_range (move missions) unsupported: empty in every supported problem */
+        for (int k = 0; k < e->nrange; k++)     /* agent_pos in target_range ('move') */
+            if (e->ax == e->range_x[k] && e->ay == e->range_y[k]) {
+                if (!e->has_reward) { e->reward = env_reward_at(e); e->has_reward = 1; }
+                e->mission_done = 1;
+                break;
+            }
     }
     if (action == A_DONE) {
         if (e->mission_done) {
@@ -839,7 +932,8 @@ static void env_step(env_t *e, int action, uint8_t img[7][7][3], double *rew, in
 #define EXPORT __attribute__((visibility("default")))
 
 EXPORT orc_vec *orc_create(int problem, int mission, int size, int num_objects, int all_doors_open,
-                           int n_envs, int64_t base_seed, int64_t index_offset, int livelock_words) {
+                           int n_envs, int64_t base_seed, int64_t index_offset, int livelock_words,
+                           int see_through_walls, int obstacles, double percent_obstacles) {
     if (size < 5 || size > MAXS || n_envs <= 0) return NULL;
     orc_vec *v = (orc_vec *)calloc(1, sizeof(orc_vec));
     v->n = n_envs;
@@ -848,6 +942,9 @@ EXPORT orc_vec *orc_create(int problem, int mission, int size, int num_objects, 
         env_t *e = &v->e[i];
         e->S = size; e->max_steps = size * size; e->problem = problem; e->cfg_mission = mission;
         e->num_objects = num_objects; e->all_doors_open = all_doors_open;
+        e->see_through_walls = see_through_walls;
+        /* range(floor((size - 2)**2 * percent_obstacles)) (custom_env.py:156) */
+        e->n_obstacles = obstacles ? (int)floor((double)((size - 2) * (size - 2)) * percent_obstacles) : 0;
         e->livelock_words = livelock_words;
         mt_seed_int(&e->mt, (uint64_t)base_seed);          /* random.seed(c.seed), custom_env.py:82 */
         e->pcg.state = (u128)(base_seed + index_offset + i); /* overwritten at first reset */

@@ -42,7 +42,8 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         L.orc_create.restype = P
-        L.orc_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
+        L.orc_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                                      ctypes.c_int, ctypes.c_int, ctypes.c_double]
         L.orc_destroy.argtypes = [P]
         L.orc_reset.argtypes = [P, ctypes.c_int64, ctypes.c_int64, P, P, P, P]
         L.orc_reset_ex.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, P, P, P, P]
@@ -66,12 +67,14 @@ class OracleVec:
 
     def __init__(self, problem="multi", mission=5, size=8, num_objects=4, n_envs=16,
                  seed=42, index_offset=0, all_doors_open=False,
-                 livelock_words=LIVELOCK_WORDS):
+                 livelock_words=LIVELOCK_WORDS, see_through_walls=True, obstacles=False,
+                 percent_obstacles=0.05):
         self.L = lib()
         self.n, self.S, self.seed, self.offset = n_envs, size, seed, index_offset
         m = -1 if mission is None else int(mission)
         self.h = self.L.orc_create(PROBLEMS[problem], m, size, num_objects, int(all_doors_open),
-                                   n_envs, seed, index_offset, livelock_words)
+                                   n_envs, seed, index_offset, livelock_words, int(see_through_walls),
+                                   int(obstacles), float(percent_obstacles))
         if not self.h:
             raise ValueError("orc_create failed")
 

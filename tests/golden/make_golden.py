@@ -242,6 +242,8 @@ def run_config(name, cfg, n, T, seed_actions=1234):
     d["meta"] = np.array([S, n, T, cfg.seed, -1 if cfg.env.mission is None else cfg.env.mission,
                           cfg.env.num_objects], np.int64)
     d["problem"] = np.array(cfg.env.problem)
+    d["env_flags"] = np.array([int(bool(cfg.env.see_through_walls)), int(bool(cfg.env.obstacles))], np.int64)
+    d["percent_obstacles"] = np.array(float(cfg.env.percent_obstacles), np.float64)
     names = sorted(missions)
     d["mission_names"] = np.array(names)
     d["mission_tokens"] = np.stack([missions[k] for k in names]) if names else np.zeros((0, 32), np.uint8)
@@ -252,8 +254,22 @@ CONFIGS = []
 for m, tag in [(5, "gtg"), (0, "gto"), (2, "pkp"), (1, "tgl"), (None, "all")]:
     for S in (8, 11, 16):
         CONFIGS.append(("multi_%s_s%d" % (tag, S), dict(problem="multi", mission=m, size=S)))
-for p in ("gtg", "gto", "pkp", "opn"):
+for p in ("gtg", "gto", "pkp", "opn", "drp", "mov", "full"):
     CONFIGS.append(("single_%s_s8" % p, dict(problem=p, mission=None, size=8)))
+# env features no shipped config enables (single.yaml:26-28): obstacles (custom_env.py:155-172)
+# and see_through_walls=False (minigrid process_vis), alone and together
+CONFIGS += [
+    ("single_full_s11", dict(problem="full", mission=None, size=11)),
+    ("single_mov_s16", dict(problem="mov", mission=None, size=16)),
+    ("obst_single_gtg_s8", dict(problem="gtg", mission=None, size=8, obstacles=True)),
+    ("obst_single_mov_s11", dict(problem="mov", mission=None, size=11, obstacles=True, percent_obstacles=0.2)),
+    ("obst_multi_all_s8", dict(problem="multi", mission=None, size=8, obstacles=True)),
+    ("obst_multi_all_s16", dict(problem="multi", mission=None, size=16, obstacles=True)),
+    ("novis_multi_all_s8", dict(problem="multi", mission=None, size=8, see_through_walls=False)),
+    ("novis_single_gto_s11", dict(problem="gto", mission=None, size=11, see_through_walls=False, num_objects=12)),
+    ("novis_obst_multi_tgl_s16", dict(problem="multi", mission=1, size=16, see_through_walls=False,
+                                      obstacles=True, percent_obstacles=0.1)),
+]
 
 
 def main():

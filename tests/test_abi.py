@@ -48,8 +48,13 @@ def test_library_is_gfx950_code_object():
 
 def test_invalid_configs_rejected_without_gpu(lib):
     from mgx import _lib
-    bad = [dict(problem=99), dict(size=3), dict(n_envs=0), dict(see_through_walls=0), dict(obstacles=1),
-           dict(mission=3), dict(num_objects=19), dict(n_stack=0), dict(problem=_lib.PROBLEMS["mov"])]
+    P = _lib.PROBLEMS
+    bad = [dict(problem=99), dict(size=3), dict(n_envs=0), dict(obstacles=1, percent_obstacles=1.5),
+           dict(mission=3), dict(num_objects=19), dict(n_stack=0),
+           # room too small for everything place_obj must place: the reference never returns
+           dict(problem=P["full"], size=7), dict(problem=P["gtg"], size=5, num_objects=8),
+           dict(problem=P["mov"], size=5, num_objects=7, obstacles=1, percent_obstacles=0.3),
+           dict(problem=P["drp"], num_objects=25)]
     for kw in bad:
         c = _lib.MgxConfig(problem=0, mission=5, size=8, num_objects=4, see_through_walls=1, n_stack=4,
                            n_envs=64, base_seed=42)
@@ -68,3 +73,5 @@ def test_mission_text_table(lib):
     assert _lib.mission_text(0 | (0 << 2) | (0 << 5)) == "go to blue door"
     assert _lib.mission_text(2 | (5 << 2) | (3 << 5)) == "pick up yellow box"
     assert _lib.mission_text(1 | (3 << 2) | (0 << 5)) == "toggle purple door"
+    assert _lib.mission_text(128) == "drop"
+    assert [_lib.mission_text(129 + d) for d in range(4)] == ["move left", "move right", "move up", "move down"]

@@ -1,5 +1,5 @@
 """HIP engine parity (needs an MI355X): libmgx through its C ABI against
-  (1) the golden fixtures made by executing the reference (all 19 configs,
+  (1) the golden fixtures made by executing the reference (every config,
       every step, every state field, every RNG position),
   (2) the SB3-layer oracle (VecTransposeImage + VecFrameStack + terminal obs),
   (3) the C oracle at 1,024 envs (bit-exact transitions),
@@ -65,6 +65,20 @@ class EngineSource:
 FIXTURES = TC.fixtures()
 
 
+@pytest.mark.parametrize("kw", [dict(problem="full", size=7), dict(problem="gtg", size=5, num_objects=8),
+                                dict(problem="mov", size=5, num_objects=7, obstacles=True, percent_obstacles=0.3),
+                                dict(problem="multi", mission=3), dict(problem="opn", num_objects=13),
+                                dict(problem="nope")])
+def test_unsatisfiable_or_invalid_configs_are_rejected(kw):
+    """Configs on which the reference raises (ValueError / AssertionError) or never returns
+    (place_obj over a room with too few free cells) are refused at create time."""
+    _need_gpu()
+    from mgx import MgxEngine
+    from mgx._lib import MgxError
+    with pytest.raises((MgxError, ValueError)):
+        MgxEngine(n_envs=64, **kw)
+
+
 @pytest.mark.parametrize("path", FIXTURES, ids=lambda p: p.split("/")[-1][:-4])
 def test_engine_matches_reference_fixture(path):
     _need_gpu()
@@ -76,7 +90,8 @@ def test_engine_matches_reference_fixture(path):
     assert msg is None, msg
 
 
-@pytest.mark.parametrize("name", ["multi_all_s8", "multi_gtg_s8", "multi_tgl_s16", "single_pkp_s8"])
+@pytest.mark.parametrize("name", ["multi_all_s8", "multi_gtg_s8", "multi_tgl_s16", "single_pkp_s8",
+                                  "single_full_s8", "obst_single_mov_s11", "novis_obst_multi_tgl_s16"])
 @pytest.mark.parametrize("ring", [(-1, 0), (2, 1), (4, 2), (8, 3)], ids=["inline", "ring2", "ring4", "ring8_every3"])
 def test_engine_reset_paths_match_fixture(name, ring):
     """Same fixtures through the other reset paths: episodes generated inline in
@@ -91,7 +106,8 @@ def test_engine_reset_paths_match_fixture(name, ring):
 
 
 @pytest.mark.parametrize("name,n_stack,mdt", [("multi_all_s8", 4, "i64"), ("multi_pkp_s11", 3, "u8"),
-                                              ("multi_tgl_s16", 1, "i64")])
+                                              ("multi_tgl_s16", 1, "i64"), ("novis_multi_all_s8", 4, "i64"),
+                                              ("novis_single_gto_s11", 2, "u8")])
 def test_frame_stack_and_terminal_obs_match_sb3_layer(name, n_stack, mdt):
     """Full stacked observation + stacked terminal_observation every step vs the
     numpy VecTransposeImage/VecFrameStack restatement fed with the fixture."""

@@ -22,8 +22,11 @@ def fixtures():
 
 def fixture_cfg(d):
     S, n, T, seed, mission, nobj = [int(x) for x in d["meta"]]
+    stw, obst = [int(x) for x in d["env_flags"]] if "env_flags" in d else (1, 0)
+    pct = float(d["percent_obstacles"]) if "percent_obstacles" in d else 0.05
     return dict(problem=str(d["problem"]), mission=None if mission < 0 else mission, size=S,
-                num_objects=nobj, n_envs=n, seed=seed), T
+                num_objects=nobj, n_envs=n, seed=seed, see_through_walls=bool(stw), obstacles=bool(obst),
+                percent_obstacles=pct), T
 
 
 def _eq(a, b):
@@ -90,7 +93,9 @@ class OracleSource:
     def __init__(self, cfg):
         import oracle as O
         self.v = O.OracleVec(cfg["problem"], cfg["mission"], cfg["size"], cfg["num_objects"], cfg["n_envs"],
-                             cfg["seed"])
+                             cfg["seed"], see_through_walls=cfg.get("see_through_walls", True),
+                             obstacles=cfg.get("obstacles", False),
+                             percent_obstacles=cfg.get("percent_obstacles", 0.05))
 
     def reset(self):
         return self.v.reset()
