@@ -58,10 +58,19 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
     ap.add_argument("--probe", type=int, default=256, help="eager steps timed per launch for the roofline")
     ap.add_argument("--workload", default="rollout", choices=["rollout", "ppo"])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
+                    help="BASELINE.json config preset (per-GPU share): 2 GTG 8x8 65,536 envs; "
+                         "4 ALL mixed 8x8 32,768 envs (256k over 8 GPUs); 5 TGL 16x16 131,072 envs (1M over 8)")
     ap.add_argument("--horizon", type=int, default=16, help="ppo: env steps per rollout")
     ap.add_argument("--batch-size", type=int, default=65536, help="ppo: minibatch size")
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
-    return ap.parse_args()
+    args = ap.parse_args()
+    presets = {2: dict(mission="5", size=8, n_envs=65536), 4: dict(mission="None", size=8, n_envs=32768),
+               5: dict(mission="1", size=16, n_envs=131072)}
+    for k, v in presets[args.config].items():          # a preset fills what was not given explicitly
+        if getattr(args, k) == ap.get_default(k):
+            setattr(args, k, v)
+    return args
 
 
 def cpu_baseline(args, seconds):
@@ -85,6 +94,17 @@ def cpu_baseline(args, seconds):
     return dict(value=n * steps / dt, unit="env-steps/s", cores=1, kind="port",
                 sample="C oracle (oracle/mgx_oracle.c), 1 thread, %d envs x %d steps (%.1fs), same config, "
                        "auto-reset included; host: %s" % (n, steps, dt, _cpu_model()))
+
+
+def _workload_name(args, mission, n, world):
+    key = (args.problem, mission, args.size)
+    if key == ("multi", 5, 8):
+        return "GTG 8x8 random-action rollout, %d envs/GPU (BASELINE config 2)" % n
+    if key == ("multi", None, 8):
+        return "ALL mixed-task 8x8 random-action rollout, %d envs/GPU, %d total (BASELINE config 4)" % (n, n * world)
+    if key == ("multi", 1, 16):
+        return "TGL 16x16 random-action rollout, %d envs/GPU, %d total (BASELINE config 5)" % (n, n * world)
+    return "%s/%s %dx%d random-action rollout, %d envs/GPU" % (args.problem, mission, args.size, args.size, n)
 
 
 def _cpu_model():
@@ -303,10 +323,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (uniform random actions on {0..6}, seed 1234+rank; env i seeded 42+i)",
-            "config": {"workload": "GTG 8x8 random-action rollout, %d envs/GPU (BASELINE config 2)" % n
-                       if (args.problem, mission, args.size) == ("multi", 5, 8) else
-                       "%s/%s %dx%d random-action rollout, %d envs/GPU" % (args.problem, mission, args.size,
-                                                                           args.size, n),
+            "config": {"workload": _workload_name(args, mission, n, world),
                        "problem": args.problem, "mission": mission, "size": args.size, "num_objects": 4,
                        "envs_per_gpu": n, "n_stack": args.n_stack, "parallelism": "env-sharded dp%d" % world,
                        "hipgraph": bool(graph is not None)},

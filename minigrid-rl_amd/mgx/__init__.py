@@ -5,6 +5,7 @@ src/custom_env.py, src/environment.py, src/ppo.py) over libmgx.so (HIP/gfx950).
 """
 from ._lib import MgxError, mission_text  # noqa: F401
 from .engine import MgxEngine, gae  # noqa: F401
+from .evaluation import EvalCallback, evaluate_policy  # noqa: F401
 from .vec_env import MgxVecEnv  # noqa: F401
 
-__all__ = ["MgxEngine", "MgxError", "MgxVecEnv", "gae", "mission_text"]
+__all__ = ["EvalCallback", "MgxEngine", "MgxError", "MgxVecEnv", "evaluate_policy", "gae", "mission_text"]

@@ -201,6 +201,12 @@ class ActorCriticPolicy(nn.Module):
         actions = dist.probs.argmax(1) if deterministic else dist.sample()
         return actions, self.value_net(vf).flatten(), dist.log_prob(actions)
 
+    @torch.no_grad()
+    def predict(self, obs, deterministic=False):
+        """SB3 BasePolicy.predict (actions only): mode of the action distribution
+        (argmax of its probs) when deterministic, else a sample."""
+        return self.forward(obs, deterministic)[0]
+
     def evaluate_actions(self, obs, actions):
         pi, vf = self._latent(obs)
         dist = torch.distributions.Categorical(logits=self.action_net(pi))

@@ -58,6 +58,7 @@ class PPOConfig:
     final_learning_rate: float = 3e-6
     optim_eps: float = 1e-8
     n_frames_stack: int = 4
+    n_eval_episodes: int = 100          # algorithm/ppo.yaml: evaluate_policy after learn (src/ppo.py:161-165)
     seed: int = 42
     adv_norm: str = "minibatch"         # "minibatch" (reference) | "global" (all-reduced stats)
     mission_cache: bool = True          # policy.py: GRU once per distinct mission stack
@@ -132,7 +133,7 @@ class RolloutCollector:
         self.last_episode_starts.fill_(1.0)
 
     @torch.no_grad()
-    def collect(self):
+    def collect(self, callback=None):
         e, pol, cfg, buf = self.engine, self.policy, self.cfg, self.buffer
         pol.train(False)
         gamma32 = torch.tensor(cfg.gamma, dtype=torch.float32)
@@ -161,6 +162,9 @@ class RolloutCollector:
             d = e.done
             ep_r.append(torch.where(d, e.ep_return, torch.nan))
             ep_l.append(torch.where(d, e.ep_len.float(), torch.nan))
+            if callback is not None:       # BaseCallback.on_step, once per vectorised step
+                callback.on_step(pol, self.num_timesteps)
+                pol.train(False)
         self.last_dones.copy_(e.done)
         last_values = pol.predict_values(e.obs)
         buf.compute_returns_and_advantage(last_values, self.last_dones, cfg.gamma, cfg.gae_lambda)
@@ -246,13 +250,16 @@ class Trainer:
         return {k: float(torch.stack(v).mean()) for k, v in stats.items()} | {"lr": lr}
 
 
-def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None):
-    """PPO(...).learn(total_timesteps) for one rank's env shard; returns (policy, history)."""
+def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None, callback=None, evaluate=False):
+    """PPO(...).learn(total_timesteps, callback=callback) for one rank's env shard; returns
+    (policy, history, engine).  evaluate=True then runs evaluate_policy(model, vec_env,
+    n_eval_episodes) on the training engine as src/ppo.py:161-165 does (history[-1]
+    gets mean_reward / std_reward)."""
     from .policy import ActorCriticPolicy
     torch.manual_seed(cfg.seed + rank)
     eng = MgxEngine(n_envs=cfg.n_envs, seed=cfg.seed, env_index_offset=rank * cfg.n_envs,
                     n_stack=cfg.n_frames_stack, terminal_mode="truncated", mission_dtype=torch.uint8,
-                    device=device, **cfg.env)
+                    device=device, reward64=True, **cfg.env)
     pol = ActorCriticPolicy(n_stack=cfg.n_frames_stack, optim_eps=cfg.optim_eps, lr=cfg.initial_learning_rate,
                             mission_cache=cfg.mission_cache).to(eng.device)
     if group is not None:   # identical initial weights on every rank
@@ -264,7 +271,7 @@ def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None):
     hist = []
     world = tr.world
     while col.num_timesteps * world < total_timesteps:
-        buf = col.collect()
+        buf = col.collect(callback)
         progress = 1.0 - float(col.num_timesteps * world) / float(total_timesteps)
         mean, std, s = tr.global_adv_stats(buf)
         st = tr.train(buf, progress)
@@ -274,5 +281,12 @@ def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None):
         hist.append(st)
         if log:
             log(st)
+    if evaluate:
+        from .evaluation import evaluate_policy
+        mean_r, std_r = evaluate_policy(pol, eng, cfg.n_eval_episodes)
+        if hist:
+            hist[-1].update(mean_reward=mean_r, std_reward=std_r)
+        if log:
+            log(dict(mean_reward=mean_r, std_reward=std_r, n_eval_episodes=cfg.n_eval_episodes))
     eng.poll_error()
     return pol, hist, eng
