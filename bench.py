@@ -12,8 +12,8 @@ Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel
 (mgx_step_kernel) with SURVEY.md §8(d)'s algorithmic bytes
   B_alg = 334*steps + (3*S^2 + 208)*resets     (per launch: one step of all N envs)
 divided by its average launch duration, measured live with HIP events on the
-launch stream around each mgx_step call that neither forks nor joins a refill
-epoch (so the event pair brackets exactly one mgx_step_kernel, which still runs
+launch stream around each run of consecutive mgx_step calls that neither fork nor join a refill epoch
+(so the event pair brackets only mgx_step_kernel launches, which still run
 concurrently with that epoch's refill, as in the timed region);
 `traffic` is the rocprofv3 PMC figure committed under profiles/.
 `cpu_baseline` times the C oracle (oracle/, single thread) on a bounded sample.
@@ -273,20 +273,31 @@ def main():
     st1 = eng.stats()
     eng.poll_error()
     # roofline probe: per-launch duration of mgx_step_kernel (HIP events on its stream)
-    probe_us = []
+    # Windows of consecutive launches that neither fork nor join a refill epoch: each
+    # bracketed by one event pair, so the per-launch figure is kernel time plus the
+    # back-to-back dispatch gap (no host latency in it).
+    windows, cur = [], None
     for t in range(P):
         if eng.epoch_boundary():
+            if cur is not None:
+                cur[1].record(stream)
+                windows.append(cur)
+                cur = None
             eng.step(actions[W + K + t])
             continue
-        a0 = torch.cuda.Event(enable_timing=True)
-        a1 = torch.cuda.Event(enable_timing=True)
-        a0.record(stream)
+        if cur is None:
+            cur = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), 0]
+            cur[0].record(stream)
         eng.step(actions[W + K + t])
-        a1.record(stream)
-        probe_us.append((a0, a1))
+        cur[2] += 1
+    if cur is not None:
+        cur[1].record(stream)
+        windows.append(cur)
     torch.cuda.synchronize(dev)
     eng.poll_error()
-    probe_us = [x.elapsed_time(y) * 1e3 for x, y in probe_us]
+    probe_us = []
+    for a0, a1, cnt in windows:
+        probe_us += [a0.elapsed_time(a1) * 1e3 / cnt] * cnt
     elapsed = torch.tensor([wall, gpu_ms / 1e3], dtype=torch.float64, device=dev)
     steps_done = torch.tensor([float(st1["steps"] - st0["steps"]), float(st1["resets"] - st0["resets"])],
                               dtype=torch.float64, device=dev)

@@ -376,47 +376,40 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
 }
 
 // =============================================================== step kernel
-// Work split helper: item w -> (list index, cell) with consecutive threads on
-// different envs; one division up front, then incremental.
-struct Split {
-    int li, c, dli, dc, n;
-    __device__ __forceinline__ Split(int w0, int stride, int nlist) : n(nlist) {
-        c = w0 / nlist; li = w0 - c * nlist;
-        dc = stride / nlist; dli = stride - dc * nlist;
-    }
-    __device__ __forceinline__ void next() { li += dli; c += dc; if (li >= n) { li -= n; c++; } }
-};
+// Grids in the step kernel's LDS are chunk-major, [GS/16][64 lanes][16 B] (the LDS-DMA
+// layout: one 16-B chunk per lane per global_load_lds); byte b of lane le's grid:
+__device__ __forceinline__ int cm_off(int le, int b) { return (b >> 4) * (BLOCK_ENVS * 16) + le * 16 + (b & 15); }
 
-// Render the 7x7 view of every listed env into its LDS frame row, spreading the
-// (env, cell) pairs over all 256 threads of the workgroup.
-__device__ __forceinline__ void render_block(const uint8_t *s_grid, uint8_t *s_fr, const uint32_t *s_rp,
-                                             const uint8_t *list, int nlist, int S, int GSL, int FSTRIDE,
-                                             int FOFF) {
-    if (nlist == 0) return;
-    const int total = nlist * 49;
-    Split sp(threadIdx.x, BLOCK_THREADS, nlist);
-    for (int w = threadIdx.x; w < total; w += BLOCK_THREADS, sp.next()) {
-        const int le = list ? list[sp.li] : sp.li;
-        const int c = sp.c;
-        const uint32_t rp = s_rp[le];
-        const int ax = rp & 0xFF, ay = (rp >> 8) & 0xFF, dir = (rp >> 16) & 3;
-        const uint8_t carry = (uint8_t)(rp >> 24);
-        const int vx = (c * 37) >> 8, vy = c - vx * 7;          // c / 7 for c < 49
-        const int dx = (dir == 0) - (dir == 2), dy = (dir == 1) - (dir == 3);
-        uint8_t code;
-        if (c == 3 * 7 + 6) {
-            code = carry ? carry : CODE_EMPTY;
-        } else {
-            const int wx = ax + (6 - vy) * dx - (vx - 3) * dy;   // right_vec = (-dy, dx)
-            const int wy = ay + (6 - vy) * dy + (vx - 3) * dx;
-            const bool in = (unsigned)wx < (unsigned)S && (unsigned)wy < (unsigned)S;
-            code = in ? s_grid[le * GSL + wy * S + wx] : CODE_WALL;
+// Render cells [13q, 13q + 13) of env slot `le`'s 7x7 view (c = vx*7 + vy; q = 3 holds the
+// last 10) into a frame row fr ([type 49][colour 49][state 49]).  The view is closed form:
+// cell (vx, vy) = A + (6 - vy) * dir_vec + (vx - 3) * right_vec (minigrid's slice + (dir+1)
+// rotate_left), out of bounds -> Wall, (3, 6) -> carried object or None.  `grids` is the
+// block's current grids or its popped episodes' grids (both chunk-major).
+// All thirteen grid bytes are read before any frame byte is written: one LDS round trip.
+__device__ __forceinline__ void render13(const uint8_t *grids, int S, int le, int q, uint32_t rp, uint8_t *fr) {
+    const int ax = rp & 0xFF, ay = (rp >> 8) & 0xFF, dir = (rp >> 16) & 3;
+    const uint8_t carry = (uint8_t)(rp >> 24);
+    const int dx = (dir == 0) - (dir == 2), dy = (dir == 1) - (dir == 3);
+    uint8_t code[13];
+#pragma unroll
+    for (int k = 0; k < 13; k++) {
+        const int c = 13 * q + k;
+        const int vx = (c * 37) >> 8, vy = c - vx * 7;                 // c / 7 for c < 52
+        const int wx = ax + (6 - vy) * dx - (vx - 3) * dy;              // right_vec = (-dy, dx)
+        const int wy = ay + (6 - vy) * dy + (vx - 3) * dx;
+        const bool in = (unsigned)wx < (unsigned)S && (unsigned)wy < (unsigned)S;
+        const uint8_t g = grids[cm_off(le, in ? wy * S + wx : 0)];
+        code[k] = c == 3 * 7 + 6 ? (carry ? carry : CODE_EMPTY) : (in ? g : CODE_WALL);
+    }
+#pragma unroll
+    for (int k = 0; k < 13; k++) {
+        const int c = 13 * q + k;
+        if (c < 49) {
+            const uint32_t v = encode3(code[k]);
+            fr[c] = (uint8_t)v;
+            fr[49 + c] = (uint8_t)(v >> 8);
+            fr[98 + c] = (uint8_t)(v >> 16);
         }
-        const uint32_t v = encode3(code);
-        uint8_t *fr = s_fr + le * FSTRIDE + FOFF;
-        fr[c] = (uint8_t)v;
-        fr[49 + c] = (uint8_t)(v >> 8);
-        fr[98 + c] = (uint8_t)(v >> 16);
     }
 }
 
@@ -432,25 +425,30 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // staged path: smem = image stacks [64][IMG] (new frame in slot 0 of a row).
     const bool fast = p.fast_roll;
     uint8_t *s_stk = smem;
-    uint8_t *s_grid = smem + p.stk_step;         // grids [64][GSL]
-    uint8_t *s_pgrid = s_grid + p.grid_lds;      // popped grids, staged [GS/16][64 lanes][16 B]
-    // popped ring slot header + RNG snapshot (LDS-DMA destinations are lane-linear; kept in the
-    // dynamic segment: hipcc 7.2 emitted no M0 setup for a static __shared__ destination)
-    uint4 *s_phdr = reinterpret_cast<uint4 *>(s_pgrid + BLOCK_ENVS * p.GS);
-    uint4 *s_tokA = s_phdr + BLOCK_ENVS;         // per lane: mission tokens 0..15 (of the mission
-    uint4 *s_tokB = s_tokA + BLOCK_ENVS;         // whose stack this step writes), tokens 16..31
+    uint8_t *s_grid = smem + p.stk_step;         // grids, chunk-major [GS/16][64 lanes][16 B] (cm_off)
+    uint8_t *s_pgrid = s_grid + BLOCK_ENVS * p.GS;   // popped episodes' grids, same layout
+    // LDS-DMA destinations are lane-linear (kept in the dynamic segment: hipcc 7.2 emitted no
+    // M0 setup for a static __shared__ destination)
+    uint4 *s_phdr = reinterpret_cast<uint4 *>(s_pgrid + BLOCK_ENVS * p.GS);   // popped ring slot header
+    uint4 *s_tokA = s_phdr + BLOCK_ENVS;         // per lane: the current mission's tokens 0..15,
+    uint4 *s_tokB = s_tokA + BLOCK_ENVS;         // 16..31 (envs whose stack is still filling)
+    uint4 *s_ptokA = s_tokB + BLOCK_ENVS;        // ... and the popped episode's mission tokens
+    uint4 *s_ptokB = s_ptokA + BLOCK_ENVS;
+    uint4 *s_prng = s_ptokB + BLOCK_ENVS;        // [2][64] the popped episode's RNG snapshot
+    uint8_t *s_tfr = reinterpret_cast<uint8_t *>(s_prng + 2 * BLOCK_ENVS);   // terminal frames [64][FROW]
     const int IMG = p.img_bytes;
     const int FSTRIDE = fast ? FROW : IMG, FOFF = fast ? 1 : 0;
     __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params ax | ay<<8 | dir<<16 | carry<<24
     __shared__ uint8_t s_done[BLOCK_ENVS];
     __shared__ uint8_t s_term[BLOCK_ENVS];       // done env whose stacked terminal_observation is written
-    __shared__ uint8_t s_dirty[BLOCK_ENVS];
     __shared__ uint8_t s_dlist[BLOCK_ENVS];      // envs that popped a new episode (render + mission lists)
     __shared__ uint8_t s_flist[BLOCK_ENVS];      // envs whose mission stack is still filling
     __shared__ uint8_t s_fslot[BLOCK_ENVS];      // ... and the slot that flips 0 -> tokens
     __shared__ uint32_t s_rp2[BLOCK_ENVS];       // render params of the popped episodes' first frames
+    __shared__ uint8_t s_popf[BLOCK_ENVS];       // env popped a new episode (its grid is in s_pgrid)
     __shared__ int s_nd, s_npop, s_nf;
     __shared__ unsigned long long s_dmask, s_tmask;   // done / terminal-written envs as bit masks
+    __shared__ unsigned long long s_dirtym;           // envs whose grid changed
     __shared__ unsigned long long s_ll;
 
     const int tid = threadIdx.x;
@@ -467,22 +465,13 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     unsigned long long ts1 = 0, ts2 = 0, tsA = 0, tsB = 0, tsC = 0;
 #endif
 
-    // ---- phase 1: issue every independent load up front --------------------------
-    // (a) this lane's env state + action (wave 0)
+    // ---- phase 1: issue every load up front (one round trip; wave 0's pop: a second) ----
     EnvState st;
     int a = 0;
     uint4 odir = make_uint4(0, 0, 0, 0);          // old direction stack (n_stack == 4: one uint4)
     uint8_t rhead = 0, rpub = 0;                  // this env's ring position and published end
     uint64_t mrange = 0;                          // 'move' target_range (problems mov / full only)
-    if (tid < ne) {
-        st = p.state[e0 + tid];
-        if (p.has_move) mrange = p.range_cur[e0 + tid];
-        a = (int)actions[e0 + tid];
-        if (p.n_stack == 4) odir = reinterpret_cast<const uint4 *>(o.dir)[e0 + tid];
-        if (p.D > 0) { rhead = p.ring_head[e0 + tid]; rpub = p.ring_pub[e0 + tid]; }
-    }
-
-    // (b) fast roll: the old image-stack dwords this lane's output quads need, into registers
+    // (a) fast roll: the old image-stack dwords this lane's output quads need, into registers
     constexpr int DW = FRAME_DW4;                                                     // 147
     constexpr int MAXQ = (BLOCK_ENVS * DW / 4 + BLOCK_THREADS - 1) / BLOCK_THREADS;  // 10
     const uint32_t *g32in = reinterpret_cast<const uint32_t *>(o.img + e0 * (int64_t)IMG);
@@ -518,26 +507,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         tq36 = g32in[kt + 36];
         if (kt + 37 < limit) tq37 = g32in[kt + 37];
     }
-    // (c) grids -> LDS (and, staged path, the whole old stacks -> LDS)
-    {
-        const int q = p.GS >> 4;
-        const int n16 = ne * q;
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.grid + e0 * p.GS);
-        for (int base = 0; base < n16; base += 4 * BLOCK_THREADS) {
-            uint4 v[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) v[j] = src[min(base + j * BLOCK_THREADS + tid, n16 - 1)];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int i = base + j * BLOCK_THREADS + tid;
-                if (i < n16) {
-                    const int e = i / q, c = i - e * q;
-                    uint32_t *d = reinterpret_cast<uint32_t *>(s_grid + e * p.GSL + c * 16);
-                    d[0] = v[j].x; d[1] = v[j].y; d[2] = v[j].z; d[3] = v[j].w;
-                }
-            }
-        }
-    }
+    // (b) staged path: the whole old stacks -> LDS
     if (!fast) {
         const uint8_t *gimg = o.img + e0 * (int64_t)IMG;
         const int nbytes = ne * IMG;
@@ -547,52 +517,67 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         for (int i = tid; i < n16; i += BLOCK_THREADS) dst[i] = src[i];
         for (int i = (n16 << 4) + tid; i < nbytes; i += BLOCK_THREADS) s_stk[i] = gimg[i];
     }
-    // Every phase-1 load has landed (the grid copy already drained them in issue order).
-    // Saying so explicitly matters: otherwise the waitcnt pass assumes a qa/qb load may be
-    // pending on some path and puts a vmcnt(0) before every roll quad, which then waits on
-    // the previous quad's STORES (vmcnt counts both) and serialises the whole roll.
+
+    // (c) env state, action, direction row and ring indices of env (tid mod 64).  Every wave
+    // loads them (three of the four copies are L2 hits) so that the loads are branch-free: a
+    // phi copy at the end of a `tid < ne` branch would force a wait before the grid DMA.
+    {
+        const int le0 = min(tid & (BLOCK_ENVS - 1), ne - 1);
+        const uint4 sv = reinterpret_cast<const uint4 *>(p.state)[e0 + le0];
+        __builtin_memcpy(&st, &sv, sizeof st);
+        a = (int)actions[e0 + le0];
+        odir = p.n_stack == 4 ? reinterpret_cast<const uint4 *>(o.dir)[e0 + le0]
+                              : reinterpret_cast<const uint4 *>(p.state)[0];      // unused
+        rhead = p.ring_head[e0 + le0];           // allocated (zeros) even without a ring
+        rpub = p.ring_pub[e0 + le0];
+        mrange = p.range_cur[p.has_move ? e0 + le0 : 0];
+    }
+    // (d) grids -> LDS by LDS-DMA (no registers, nothing to wait on before the barrier):
+    // wave w moves chunks w, w+4, ... of all 64 envs, one env per lane.  After the register
+    // loads: hipcc waits vmcnt(0) at the next use of a register load while an LDS-DMA is in
+    // flight, which would serialise them.
+    {
+        const int lane = tid & (BLOCK_ENVS - 1);
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.grid + (e0 + min(lane, ne - 1)) * p.GS);
+        for (int c = tid >> 6; c < (p.GS >> 4); c += BLOCK_THREADS / 64)
+            __builtin_amdgcn_global_load_lds(src + c, s_grid + c * (BLOCK_ENVS * 16), 16, 0, 0);
+    }
+    // (e) wave 0: SubprocVecEnv auto-reset, speculatively.  A step can end the episode only
+    // on 'forward' (goal / lava ahead), on 'done' or at the time limit, which the state and
+    // the action alone tell; for those envs the next pre-generated episode (header, tokens,
+    // grid, RNG snapshot) is fetched now, in a second round trip of this phase, and used only
+    // if the step does end it.  Envs whose stack is still filling fetch their mission's tokens.
+    bool spec = false;
+    if (tid < ne) {
+        if (st.frames < p.n_stack) {
+            const uint4 *t = reinterpret_cast<const uint4 *>(p.mtok + st.mission_id * 32);
+            __builtin_amdgcn_global_load_lds(t, s_tokA, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(t + 1, s_tokB, 16, 0, 0);
+        }
+        spec = p.D > 0 && (a == A_FORWARD || a == A_DONE || st.step_count + 1 >= S * S) &&
+               (uint8_t)(rpub - rhead) != 0;
+        if (spec) {
+            const int64_t slot = (e0 + tid) * p.D + (rhead & (p.D - 1));
+            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot, s_phdr, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 1, s_ptokA, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 2, s_ptokB, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot, s_prng, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot + 1, s_prng + BLOCK_ENVS, 16, 0, 0);
+            const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
+            for (int c = 0; c < (p.GS >> 4); c++)
+                __builtin_amdgcn_global_load_lds(gsrc + c, s_pgrid + c * (BLOCK_ENVS * 16), 16, 0, 0);
+        }
+        // (no register load here: its phi copy after the branch would wait on the DMA above)
+    }
+    // Every phase-1 load of this wave has landed (register loads and LDS-DMA alike).  Saying
+    // so explicitly matters: otherwise the waitcnt pass assumes a qa/qb load may be pending
+    // on some path and puts a vmcnt(0) before every roll quad of phase 3, which then waits
+    // on the previous quad's STORES (vmcnt counts both) and serialises the whole roll.
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 #ifdef MGX_STAMPS
     ts1 = __builtin_amdgcn_s_memtime();
 #endif
-    // ---- phase 1b (fast roll, pass 1): store the shifted OLD part of every row now
-    // (output dword j <= 109 of a row = old dwords j+36, j+37 aligned by 3 bytes), as if
-    // no env were done.  The old dwords are in registers (loaded before the barrier
-    // above), so these stores drain while wave 0 runs the step logic and the block
-    // renders.  Pass 2 (phase 3) writes what depends on this step: the new frame
-    // (j >= 110) and the zeroed old part of done envs.
-    // Waves 1-3 store now; wave 0 (the env lanes) stores its share after its ring pop,
-    // whose loads must not queue behind stores.
-    auto roll_pass1 = [&]() {
-        uint32_t *g32 = reinterpret_cast<uint32_t *>(o.img + e0 * (int64_t)IMG);
-        uint4 *g128 = reinterpret_cast<uint4 *>(g32);
-#pragma unroll
-        for (int r = 0; r < MAXQ; r++) {
-            const int q = r * BLOCK_THREADS + tid, k = 4 * q;
-            if (q < nq) {
-                const uint32_t src[5] = {qa[r].x, qa[r].y, qa[r].z, qa[r].w, qb[r]};
-                int j = k - (k / DW) * DW;
-                uint32_t w[4];
-                bool ok[4];
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    ok[t] = j <= 109;
-                    w[t] = __builtin_amdgcn_alignbyte(src[t + 1], src[t], 3);
-                    if (++j == DW) j = 0;
-                }
-                if (ok[0] && ok[1] && ok[2] && ok[3]) {
-                    if (!(MGX_DIAG_SKIP & 1)) stk_store(g128 + q, make_uint4(w[0], w[1], w[2], w[3]));
-                } else {
-#pragma unroll
-                    for (int t = 0; t < 4; t++)
-                        if (!(MGX_DIAG_SKIP & 1)) if (ok[t]) g32[k + t] = w[t];
-                }
-            }
-        }
-        // tail dword of a partial block: written in pass 2 only
-    };
-    if (fast && tid >= BLOCK_ENVS) roll_pass1();
 
     // ---- phase 2a: one lane per env: MiniGridEnv.step + PlaygroundEnv.step
     uint32_t my_err = 0;
@@ -602,16 +587,20 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     if (tid < ne) {
         const int64_t e = e0 + tid;
         if ((unsigned)a > 6u) { my_err |= MGX_DEVERR_BAD_ACTION; a = -1; }
-        uint8_t *g = s_grid + tid * p.GSL;
         const int ms = S * S;
         const int sc = st.step_count + 1;
         int ax = st.ax, ay = st.ay;
         dir = st.dir;
         uint8_t carry = st.carry;
         const int fx = ax + ((dir == 0) - (dir == 2)), fy = ay + ((dir == 1) - (dir == 3));
-        uint8_t *fp = g + fy * S + fx;
+        uint8_t *fp = s_grid + cm_off(tid, fy * S + fx);
         const uint8_t fc = *fp;
         const int ft = fc & 15;
+        // the episode ends (auto-reset) exactly when one of these holds; each implies `spec`,
+        // so the next episode is already in LDS (phase 1c)
+        const bool done_e = (a == A_FORWARD && (ft == T_GOAL || ft == T_LAVA)) || a == A_DONE || sc >= ms;
+        const bool avail = done_e && spec;
+        const bool filling = !done_e && st.frames < p.n_stack;
         double rew = 0.0;
         switch (a) {                                   // MiniGridEnv.step (3P)
             case A_LEFT: dir = (dir + 3) & 3; break;
@@ -688,35 +677,15 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             else
                 dir_stack_roll(o.dir, o.t_dir, e, p.n_stack, dir);
             write_mission_stack(o.t_mis, p.mission64, e, p.n_stack, frames, p.mtok + st.mission_id * 32);
+            // leave no load of this rare path pending in the waitcnt pass's view: otherwise it
+            // puts a vmcnt(0) (which waits on every STORE in flight) before the mission writer
+            __builtin_amdgcn_s_waitcnt(0);
         }
-        // SubprocVecEnv auto-reset: pop the next pre-generated episode.  Its loads go out
-        // before this lane's other stores (LDS-DMA, no registers).
-        const bool avail = done && p.D > 0 && (uint8_t)(rpub - rhead) != 0;
-        const bool filling = !done && st.frames < p.n_stack;
-        uint4 rng0 = make_uint4(0, 0, 0, 0), rng1 = rng0;
-        uint64_t nrange = 0;
-        if (avail) {
-            const int64_t slot = e * p.D + (rhead & (p.D - 1));
-            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot, s_phdr, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 1, s_tokA, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 2, s_tokB, 16, 0, 0);
-            const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
-            for (int c = 0; c < (p.GS >> 4); c++)          // popped grid -> staging [chunk][lane]
-                __builtin_amdgcn_global_load_lds(gsrc + c, s_pgrid + c * (BLOCK_ENVS * 16), 16, 0, 0);
-            rng0 = p.ring_rng[2 * slot];
-            rng1 = p.ring_rng[2 * slot + 1];
-            if (p.has_move) nrange = p.ring_range[slot];
-        } else if (filling) {                               // tokens of the mission that stays
-            const uint4 *t = reinterpret_cast<const uint4 *>(p.mtok + st.mission_id * 32);
-            __builtin_amdgcn_global_load_lds(t, s_tokA, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(t + 1, s_tokB, 16, 0, 0);
-        }
-        __builtin_amdgcn_s_waitcnt(0);                      // one round trip, nothing else outstanding
         if (avail) {
             const uint4 h = s_phdr[tid];
-            p.cur_rng[2 * e] = rng0;
-            p.cur_rng[2 * e + 1] = rng1;
-            if (p.has_move) p.range_cur[e] = nrange;
+            p.cur_rng[2 * e] = s_prng[tid];
+            p.cur_rng[2 * e + 1] = s_prng[BLOCK_ENVS + tid];
+            if (p.has_move) p.range_cur[e] = p.ring_range[e * p.D + (rhead & (p.D - 1))];
             new_head = (int)(uint8_t)(rhead + 1);   // published after a barrier, loads consumed
             const int nax = h.x & 0xFF, nay = (h.x >> 8) & 0xFF, ndir = (h.x >> 16) & 0xFF;
             const uint8_t mid = (uint8_t)(h.y >> 16);
@@ -767,11 +736,12 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         }
         s_done[tid] = done;
         s_term[tid] = tw;
+        s_popf[tid] = popped;
     } else if (tid < BLOCK_ENVS) {
         s_done[tid] = 0;
         s_term[tid] = 0;
+        s_popf[tid] = 0;
     }
-    if (fast && tid < BLOCK_ENVS) roll_pass1();        // wave 0's share of the early roll stores
     if (tid < BLOCK_ENVS) {                            // wave 0: ballot compaction of the lists
         const unsigned long long fm = __ballot(fill), dm = __ballot(done), pm = __ballot(popped);
         const unsigned long long tm = __ballot(tid < ne && s_term[tid]);
@@ -784,76 +754,86 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
 #ifdef MGX_STAMPS
     tsA = __builtin_amdgcn_s_memtime();
 #endif
-    // ---- phase 2b: render every env's frame (all 256 threads)
-    render_block(s_grid, s_stk, s_rp, nullptr, ne, S, p.GSL, FSTRIDE, FOFF);
-    __syncthreads();
-    if (p.vis) {                                       // see_through_walls=False: process_vis
-        if (tid < ne) apply_vis(s_stk + tid * FSTRIDE + FOFF);
-        __syncthreads();
-    }
-#ifdef MGX_STAMPS
-    tsB = __builtin_amdgcn_s_memtime();
-#endif
-
-    // ---- phase 2c: done envs: newest slot of the terminal stack, popped grids into place
-    const int nd = s_nd;
-    if (nd) {
-        if (tid < ne && done) {
-            if (s_term[tid]) {                         // the terminal frame (older frames: phase 3)
-                const int64_t e = e0 + tid;
-                uint8_t *t = o.t_img + e * (int64_t)IMG;
-                const uint8_t *fr = s_stk + tid * FSTRIDE + FOFF;
-                if (!fast) {
-                    const uint8_t *old = s_stk + tid * IMG;
-                    for (int off = 0; off < IMG - FRAME; off++) t[off] = old[off + FRAME];
-                }
-                for (int k = 0; k < FRAME; k++) t[IMG - FRAME + k] = fr[k];
-            }
-            if (popped) {                              // staged popped grid -> this env's grid row
-                uint32_t *d = reinterpret_cast<uint32_t *>(s_grid + tid * p.GSL);
-                for (int c = 0; c < (p.GS >> 4); c++) {
-                    const uint32_t *q = reinterpret_cast<const uint32_t *>(s_pgrid + c * (BLOCK_ENVS * 16) + tid * 16);
-                    d[4 * c] = q[0]; d[4 * c + 1] = q[1]; d[4 * c + 2] = q[2]; d[4 * c + 3] = q[3];
-                }
-            }
-        }
-        __syncthreads();
-        // first frames of the new episodes -> frame rows (phase 3 zero-fills the older slots)
-        render_block(s_grid, s_stk, s_rp2, s_dlist, s_npop, S, p.GSL, FSTRIDE, FOFF);
-        if (p.vis) {
-            __syncthreads();
-            if (tid < s_npop) apply_vis(s_stk + s_dlist[tid] * FSTRIDE + FOFF);
-        }
-    }
-    __syncthreads();
-    // mission stacks, block-cooperative and coalesced: fresh stacks of popped envs
-    // (zeros + tokens in the newest slot), then the one flipping slot of filling envs
+    // ---- phase 2b: mission stacks first (their stores drain during the render), block-
+    // cooperative and coalesced: fresh stacks of popped envs (zeros + tokens in the newest
+    // slot), then the one flipping slot of filling envs
     {
         const int K = p.n_stack, CPS = p.mission64 ? 16 : 2, per = K * CPS;
-        const uint8_t *tA = reinterpret_cast<const uint8_t *>(s_tokA), *tB = reinterpret_cast<const uint8_t *>(s_tokB);
+        const uint8_t *tA = reinterpret_cast<const uint8_t *>(s_ptokA), *tB = reinterpret_cast<const uint8_t *>(s_ptokB);
         const int tot_d = s_npop * per;
         for (int w = tid; w < tot_d; w += BLOCK_THREADS) {
             const int i = w / per, j = w - i * per;
             const int le = s_dlist[i], sl = j / CPS, c = j - sl * CPS;
             if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk2(o.mis, p.mission64, e0 + le, K, sl, c, tA + le * 16, tB + le * 16, sl != K - 1);
         }
-        const int tot_f = s_nf * CPS;
+        tA = reinterpret_cast<const uint8_t *>(s_tokA);
+        tB = reinterpret_cast<const uint8_t *>(s_tokB);
+        // int64: the flipping slot (256 B, whole lines); u8: the whole row (one line at n_stack
+        // 4; a 32-B slot alone would be a partial-line write)
+        const int perf = p.mission64 ? CPS : per, tot_f = s_nf * perf;
         for (int w = tid; w < tot_f; w += BLOCK_THREADS) {
-            const int i = w / CPS, c = w - i * CPS;
-            const int le = s_flist[i];
-            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk2(o.mis, p.mission64, e0 + le, K, s_fslot[le], c, tA + le * 16, tB + le * 16, false);
+            const int i = w / perf, j = w - i * perf;
+            const int le = s_flist[i], fs = s_fslot[le];
+            const int sl = p.mission64 ? fs : j / CPS, c = p.mission64 ? j : j - (j / CPS) * CPS;
+            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk2(o.mis, p.mission64, e0 + le, K, sl, c, tA + le * 16, tB + le * 16, sl < fs);
         }
     }
-    if (tid < BLOCK_ENVS) s_dirty[tid] = dirty;
+    // ---- phase 2c: one render pass for the whole block (all 256 threads, 4 per env): the
+    // newest frame of every env -- the first frame of the new episode where one was popped
+    // (rendered straight from its staged grid) -- plus the terminal frame of every env whose
+    // stacked terminal_observation is written (the finished episode's post-step view).
+    {
+        const int le = tid >> 2, q = tid & 3;
+        if (le < ne) {
+            const bool pop = s_popf[le];
+            render13(pop ? s_pgrid : s_grid, S, le, q, pop ? s_rp2[le] : s_rp[le], s_stk + le * FSTRIDE + FOFF);
+            if (s_term[le]) render13(s_grid, S, le, q, s_rp[le], s_tfr + le * FROW);
+        }
+    }
+    __syncthreads();
+    if (p.vis) {                                       // see_through_walls=False: process_vis
+        if (tid < ne) apply_vis(s_stk + tid * FSTRIDE + FOFF);
+        else if (tid >= BLOCK_ENVS && tid < BLOCK_ENVS + ne && s_term[tid - BLOCK_ENVS])
+            apply_vis(s_tfr + (tid - BLOCK_ENVS) * FROW);
+        __syncthreads();
+    }
+#ifdef MGX_STAMPS
+    tsB = __builtin_amdgcn_s_memtime();
+#endif
+    const int nd = s_nd;
+    // ---- phase 2d: newest slot (and, staged path, the older slots) of each written
+    // terminal_observation; the fast path writes the older slots in phase 3 from registers
+    if (s_tmask) {
+        const int le = tid >> 2, q = tid & 3;
+        if (le < ne && s_term[le]) {
+            uint8_t *t = o.t_img + (e0 + le) * (int64_t)IMG;
+            const uint8_t *fr = s_tfr + le * FROW;
+            for (int k = 37 * q; k < min(37 * q + 37, FRAME); k++) t[IMG - FRAME + k] = fr[k];
+            if (!fast) {
+                const uint8_t *old = s_stk + le * IMG;
+                for (int off = q; off < IMG - FRAME; off += 4) t[off] = old[off + FRAME];
+            }
+        }
+    }
+    if (tid < BLOCK_ENVS) {
+        const unsigned long long dm = __ballot(dirty);
+        if (tid == 0) s_dirtym = dm;
+    }
     if (my_err) atomicOr(p.err, my_err);
     __syncthreads();
-    if (new_head >= 0) p.ring_head[e0 + tid] = (uint8_t)new_head;   // the refill may now reuse the slot
+    // ring heads: the popped slot is consumed (its DMA landed in phase 1), so the refill may
+    // reuse it.  Every lane writes its head, changed or not: one 64-B store per block instead
+    // of a byte store per popped env.
+    if (tid < ne && p.D > 0) p.ring_head[e0 + tid] = (uint8_t)(new_head >= 0 ? new_head : rhead);
 #ifdef MGX_STAMPS
     ts2 = __builtin_amdgcn_s_memtime();
 #endif
 
     // ---- phase 3: roll the image stacks.  out byte o of an env row = its old byte o+147
     // (o < IMG-147) or the newest frame (o >= IMG-147); done envs: zeros + newest frame.
+    // Every quad is stored once, here: an earlier version stored the rows' old part right
+    // after phase 1 and the rest here, so the 128-B lines across each row's seam were written
+    // in two halves far apart in time; on MI355X that took 36 us per step instead of 27.
     if (fast) {
         // Block-relative output dword k needs old dwords k+36, k+37 (alignbyte by 3) while its
         // env column j = k mod 147 <= 109; dword 110 mixes old byte 587 with new bytes 0..2;
@@ -867,10 +847,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         for (int r = 0; r < MAXQ; r++) {
             const int q = r * BLOCK_THREADS + tid, k = 4 * q;
             const int e0q = k / DW, j0 = k - e0q * DW;
-            // envs this quad touches (it straddles at most one row boundary)
-            const unsigned long long qm = (3ull << e0q) & ((j0 >= DW - 3) ? ~0ull : (1ull << e0q));
-            const bool need = q < nq && (j0 >= 107 || (dmask & qm));
-            if (need) {                              // else pass 1 already stored this quad as-is
+            if (q < nq) {
                 // Branch-free: the 4 frame-row dwords are read together (one LDS round trip),
                 // then each output dword is a select of old / mixed / new.
                 const uint32_t src[5] = {qa[r].x, qa[r].y, qa[r].z, qa[r].w, qb[r]};
@@ -951,7 +928,20 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     tsC = __builtin_amdgcn_s_memtime();
 #endif
     // ---- phase 5: write back grids that changed (moves, pickups, resets)
-    if (!(MGX_DIAG_SKIP & 16)) grid_copy_out(p.grid + e0 * p.GS, s_grid, ne, p.GS, p.GSL, s_dirty);
+    // (a popped env's new grid is in the staging area; both chunk-major)
+    // At line granularity: grids smaller than a 128-B line are written for every env of a
+    // line with a dirty grid, so that no line is written in part.
+    if (!(MGX_DIAG_SKIP & 16)) {
+        const int q16 = p.GS >> 4;
+        const int epl = p.GS < 128 ? 128 / p.GS : 1;          // envs per line (GS is a multiple of 16)
+        const unsigned long long dirtym = s_dirtym;
+        uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * p.GS);
+        for (int i = tid; i < ne * q16; i += BLOCK_THREADS) {
+            const int e = i / q16, c = i - e * q16;
+            if (!((dirtym >> (e & ~(epl - 1))) & ((1ull << epl) - 1))) continue;
+            dst[i] = *reinterpret_cast<const uint4 *>((s_popf[e] ? s_pgrid : s_grid) + c * (BLOCK_ENVS * 16) + e * 16);
+        }
+    }
     if (tid == 0) {
         // workgroup-private stats slot: fire-and-forget adds (no load on the kernel's tail)
         atomicAdd(&p.blk[blockIdx.x].x, (unsigned long long)ne);
@@ -1517,7 +1507,9 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.cap = h->cfg.refill_cap;
     p.initial_fill = 0;
     p.mission64 = cfg->mission_int64;
-    h->lds_step = (size_t)p.stk_step + (size_t)p.grid_lds + (size_t)BLOCK_ENVS * (GS + 48);   // + popped slot staging
+    h->lds_step = (size_t)p.stk_step + (size_t)BLOCK_ENVS * 2 * GS   // grids + popped grids (chunk-major)
+                  + (size_t)BLOCK_ENVS * 7 * 16                       // + popped header, 2x2 token halves, RNG snapshot
+                  + (size_t)BLOCK_ENVS * FROW;                        // + terminal frames
     h->lds_reset = (size_t)p.stk_lds + (size_t)p.grid_lds;
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
