@@ -7,7 +7,7 @@ mkdir -p $R/gpurun_out
 timeout -k 10 600 python -m pytest tests -m gpu -q -x -rf > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
 for v in "" 2; do
-  MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_stamps$v.so timeout -k 10 200 python tests/_diag_phases.py > gpurun_out/diag$v.log 2>&1
+  MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_stamps$v.so timeout -k 10 200 python tools/_diag_phases.py > gpurun_out/diag$v.log 2>&1
   tail -1 gpurun_out/diag$v.log
 done
 timeout -k 10 300 python bench.py --steps 2048 --warmup 128 --cpu-seconds 0 > gpurun_out/bench.json 2>gpurun_out/bench.err

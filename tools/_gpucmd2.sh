@@ -5,9 +5,9 @@ R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 timeout -k 10 600 python -m pytest tests -m gpu -q -x -rf > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
-N=512 MGX_SERIAL_REFILL=1 MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_stamps3.so timeout -k 10 200 python tests/_diag_phases.py > gpurun_out/diag3_512.log 2>&1
+N=512 MGX_SERIAL_REFILL=1 MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_stamps3.so timeout -k 10 200 python tools/_diag_phases.py > gpurun_out/diag3_512.log 2>&1
 tail -1 gpurun_out/diag3_512.log
-MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_stamps3.so timeout -k 10 200 python tests/_diag_phases.py > gpurun_out/diag3.log 2>&1
+MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_stamps3.so timeout -k 10 200 python tools/_diag_phases.py > gpurun_out/diag3.log 2>&1
 tail -1 gpurun_out/diag3.log
 timeout -k 10 300 python bench.py --steps 2048 --warmup 128 --cpu-seconds 0 > gpurun_out/bench.json 2>gpurun_out/bench.err
 cat gpurun_out/bench.json
