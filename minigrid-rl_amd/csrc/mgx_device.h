@@ -224,8 +224,7 @@ constexpr int MT_WG = 16;           // groups per lane-private LDS window (160 w
 constexpr int WIN_STRIDE = 34;      // dwords per lane window row: 8-B aligned, 2-way banked for b64
 constexpr uint64_t MT_REP = 0x041041041041041ull;   // 1 in every 6-bit slot of ten
 constexpr uint64_t MT_LOW60 = (1ull << 60) - 1ull;
-constexpr int MAX_OBJS = 32;
-constexpr int OBJ_STRIDE = 33;    // words per lane objs list (odd, same reason)
+constexpr int MAX_OBJS = 32;     // objs list capacity bound; the list is sized per config (KParams.obj_cap)
 constexpr int SAT_PROBE = 64;     // rejections before the exhaustive satisfiability probe
 constexpr uint32_t PCG_LOOP_LIMIT = 1u << 20;
 

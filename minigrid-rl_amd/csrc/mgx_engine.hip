@@ -32,6 +32,11 @@ using namespace mgx;
 
 namespace {
 
+// Co-residency budget (per CU, while a refill epoch runs beside the steps): one refill wave per
+// SIMD plus three step workgroups.  VGPRs per SIMD lane: 176 + 3 x 112 = 512 (granule 8), so
+// the step kernel must stay at <= 112 VGPRs and the refill at <= 176.  LDS: 4 x refill
+// (17.4 KB at the BASELINE configs) + 3 x step (25.8 KB) <= 160 KB.  Check with
+// `make resource-usage` after any change to either kernel.
 #ifndef MGX_DIAG_SKIP
 #define MGX_DIAG_SKIP 0     // diagnostics only: skip store classes (1 pass-1, 2 pass-2, 4 missions, 16 grids)
 #endif
@@ -41,7 +46,8 @@ constexpr int BLOCK_THREADS = 256;
 constexpr int FRAME = 147;                 // 3 x 7 x 7
 constexpr int FRAME_DW4 = 147;             // dwords per env row at n_stack == 4 (588 B)
 constexpr int FROW = 148;                  // LDS frame row (fast roll): byte 0 pad, bytes 1..147 frame
-constexpr int SCRATCH_PER_ENV = WIN_STRIDE * 4 + OBJ_STRIDE * 4;   // LDS bytes per resetting lane
+// LDS bytes per resetting lane: MT window + objs list (obj_stride words, see mgx_create)
+__host__ __device__ constexpr int scratch_per_env(int obj_stride) { return WIN_STRIDE * 4 + obj_stride * 4; }
 
 struct KParams {
     EnvState *state;
@@ -56,6 +62,7 @@ struct KParams {
     int64_t n;
     int64_t seed_base;              // base_seed + env_index_offset
     int S, GS, GSL, grid_lds, n_stack, img_bytes, stk_lds, stk_step, problem, cfg_mission, num_objects, all_doors_open;
+    int obj_cap, obj_stride;        // generator objs list: capacity for this config, LDS words per lane (odd)
     uint32_t llw;
     int terminal_mode, mission64, fast_roll;
     int n_obstacles;        // floor((S-2)^2 * percent_obstacles) when cfg.obstacles (custom_env.py:156)
@@ -238,7 +245,7 @@ __device__ __forceinline__ void load_gen(Gen<NW> &G, const KParams &p, int64_t e
     G.tlen = p.tlen;
     // lane >= 0: workgroup LDS layout [64 windows][64 objs lists]; lane < 0: one env's private block
     G.win = reinterpret_cast<uint64_t *>(scratch + (lane >= 0 ? lane * (WIN_STRIDE * 4) : 0));
-    G.objs = reinterpret_cast<uint32_t *>(scratch + (lane >= 0 ? BLOCK_ENVS * (WIN_STRIDE * 4) + lane * (OBJ_STRIDE * 4)
+    G.objs = reinterpret_cast<uint32_t *>(scratch + (lane >= 0 ? BLOCK_ENVS * (WIN_STRIDE * 4) + lane * (p.obj_stride * 4)
                                                                : WIN_STRIDE * 4));
     G.llw = p.llw;
     G.err = 0;
@@ -345,6 +352,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
         G.gbase = ~0ull >> 1;
         ResetOut R;
         reset_env<NW, EXT>(G, R);
+        if (G.nobjs > p.obj_cap) G.err |= 8u;   // objs list ran past its per-config capacity
         st.ax = (uint8_t)G.ax; st.ay = (uint8_t)G.ay; st.dir = (uint8_t)G.adir; st.carry = 0;
         st.step_count = 0;
         st.tx = R.tx; st.ty = R.ty; st.target_action = R.ta; st.mission_id = R.mission_id;
@@ -435,7 +443,6 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     uint4 *s_ptokA = s_tokB + BLOCK_ENVS;        // ... and the popped episode's mission tokens
     uint4 *s_ptokB = s_ptokA + BLOCK_ENVS;
     uint4 *s_prng = s_ptokB + BLOCK_ENVS;        // [2][64] the popped episode's RNG snapshot
-    uint8_t *s_tfr = reinterpret_cast<uint8_t *>(s_prng + 2 * BLOCK_ENVS);   // terminal frames [64][FROW]
     const int IMG = p.img_bytes;
     const int FSTRIDE = fast ? FROW : IMG, FOFF = fast ? 1 : 0;
     __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params ax | ay<<8 | dir<<16 | carry<<24
@@ -778,41 +785,59 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk2(o.mis, p.mission64, e0 + le, K, sl, c, tA + le * 16, tB + le * 16, sl < fs);
         }
     }
+    // ---- phase 2c (rare, block-uniform): the terminal frame of every env whose stacked
+    // terminal_observation is written (the finished episode's post-step view) is rendered
+    // into the env's newest-frame LDS slot -- free until the render below -- and copied out
+    // as the terminal stack's newest slot.  No LDS of its own: the step kernel's LDS is what
+    // keeps three of its workgroups co-resident with the refill's waves on a CU.
+    if (s_tmask) {
+        {
+            const int le = tid >> 2, q = tid & 3;
+            if (le < ne && s_term[le]) render13(s_grid, S, le, q, s_rp[le], s_stk + le * FSTRIDE + FOFF);
+        }
+        __syncthreads();
+        if (p.vis) {
+            if (tid < ne && s_term[tid]) apply_vis(s_stk + tid * FSTRIDE + FOFF);
+            __syncthreads();
+        }
+        {
+            const int le = tid >> 2, q = tid & 3;
+            if (le < ne && s_term[le]) {
+                const uint8_t *fr = s_stk + le * FSTRIDE + FOFF;
+                uint8_t *t = o.t_img + (e0 + le) * (int64_t)IMG + (IMG - FRAME);
+#pragma unroll 1
+                for (int k = 37 * q; k < min(37 * q + 37, FRAME); k++) t[k] = fr[k];
+            }
+        }
+        __syncthreads();
+    }
     // ---- phase 2c: one render pass for the whole block (all 256 threads, 4 per env): the
     // newest frame of every env -- the first frame of the new episode where one was popped
-    // (rendered straight from its staged grid) -- plus the terminal frame of every env whose
-    // stacked terminal_observation is written (the finished episode's post-step view).
+    // (rendered straight from its staged grid).
     {
         const int le = tid >> 2, q = tid & 3;
         if (le < ne) {
             const bool pop = s_popf[le];
             render13(pop ? s_pgrid : s_grid, S, le, q, pop ? s_rp2[le] : s_rp[le], s_stk + le * FSTRIDE + FOFF);
-            if (s_term[le]) render13(s_grid, S, le, q, s_rp[le], s_tfr + le * FROW);
         }
     }
     __syncthreads();
     if (p.vis) {                                       // see_through_walls=False: process_vis
         if (tid < ne) apply_vis(s_stk + tid * FSTRIDE + FOFF);
-        else if (tid >= BLOCK_ENVS && tid < BLOCK_ENVS + ne && s_term[tid - BLOCK_ENVS])
-            apply_vis(s_tfr + (tid - BLOCK_ENVS) * FROW);
         __syncthreads();
     }
 #ifdef MGX_STAMPS
     tsB = __builtin_amdgcn_s_memtime();
 #endif
     const int nd = s_nd;
-    // ---- phase 2d: newest slot (and, staged path, the older slots) of each written
-    // terminal_observation; the fast path writes the older slots in phase 3 from registers
-    if (s_tmask) {
+    // ---- phase 2d (staged path): the older slots of each written terminal_observation
+    // (the fast path writes them in phase 3 from registers)
+    if (s_tmask && !fast) {
         const int le = tid >> 2, q = tid & 3;
         if (le < ne && s_term[le]) {
             uint8_t *t = o.t_img + (e0 + le) * (int64_t)IMG;
-            const uint8_t *fr = s_tfr + le * FROW;
-            for (int k = 37 * q; k < min(37 * q + 37, FRAME); k++) t[IMG - FRAME + k] = fr[k];
-            if (!fast) {
-                const uint8_t *old = s_stk + le * IMG;
-                for (int off = q; off < IMG - FRAME; off += 4) t[off] = old[off + FRAME];
-            }
+            const uint8_t *old = s_stk + le * IMG;
+            for (int off = q; off < IMG - FRAME; off += 4) t[off] = old[off + FRAME];
         }
     }
     if (tid < BLOCK_ENVS) {
@@ -986,6 +1011,7 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
         load_rng(G, p, e);
         ResetOut R;
         reset_env<NW, EXT>(G, R);
+        if (G.nobjs > p.obj_cap) G.err |= 8u;   // objs list ran past its per-config capacity
         store_rng(G, p, e);
         rng_snapshot(G, p.cur_rng + 2 * e);
         {
@@ -1072,6 +1098,7 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
                 G.abort = false;
                 mt_sync(G);
                 gen_attempt<NW, EXT>(G, R);
+                if (G.nobjs > p.obj_cap) G.err |= 8u;
                 if (G.abort && ++livelocks <= 100000) continue;
                 if (G.abort) G.err |= 4u;           // give up on this env (reported, never silent)
                 R.livelocks = livelocks;
@@ -1460,7 +1487,14 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.GSL = GS + 4;
     p.n_stack = cfg->n_stack;
     p.img_bytes = IMG;
-    const int scratch = BLOCK_ENVS * SCRATCH_PER_ENV;
+    // objs list capacity: multi = doors (<= 4) + goal + keys (<= 4) + objects (the lower-left
+    // room of the 3/4-room layouts reuses the upper-left counter, Q1: <= 2 x num_objects);
+    // single room = objects (24 for 'full') + goal.  Sized per config: the refill's LDS
+    // per wave decides how many step workgroups fit beside it on a CU.
+    p.obj_cap = std::min(MAX_OBJS, cfg->problem == MGX_PROBLEM_MULTI ? 9 + 2 * cfg->num_objects
+                                   : (cfg->problem == MGX_PROBLEM_FULL ? 24 : cfg->num_objects) + 1);
+    p.obj_stride = p.obj_cap | 1;
+    const int scratch = BLOCK_ENVS * scratch_per_env(p.obj_stride);
     p.stk_lds = (std::max(BLOCK_ENVS * IMG, scratch) + 15) & ~15;   // reset kernel: stack area doubles as scratch
     p.grid_lds = (BLOCK_ENVS * (GS + 4) + 15) & ~15;
     p.fast_roll = cfg->n_stack == 4;
@@ -1508,8 +1542,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.initial_fill = 0;
     p.mission64 = cfg->mission_int64;
     h->lds_step = (size_t)p.stk_step + (size_t)BLOCK_ENVS * 2 * GS   // grids + popped grids (chunk-major)
-                  + (size_t)BLOCK_ENVS * 7 * 16                       // + popped header, 2x2 token halves, RNG snapshot
-                  + (size_t)BLOCK_ENVS * FROW;                        // + terminal frames
+                  + (size_t)BLOCK_ENVS * 7 * 16;                      // + popped header, 2x2 token halves, RNG snapshot
     h->lds_reset = (size_t)p.stk_lds + (size_t)p.grid_lds;
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
@@ -1522,7 +1555,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     MGX_SET_LDS1((K<1, false>), bytes); MGX_SET_LDS1((K<2, false>), bytes); MGX_SET_LDS1((K<4, false>), bytes); \
     MGX_SET_LDS1((K<1, true>), bytes); MGX_SET_LDS1((K<2, true>), bytes); MGX_SET_LDS1((K<4, true>), bytes)
     MGX_SET_LDS(mgx_reset_kernel, h->lds_reset);
-    h->lds_refill = (size_t)((64 * (GS + 4) + 15) & ~15) + (size_t)64 * SCRATCH_PER_ENV;
+    h->lds_refill = (size_t)((64 * (GS + 4) + 15) & ~15) + (size_t)64 * scratch_per_env(p.obj_stride);
     MGX_SET_LDS(mgx_refill_kernel, h->lds_refill);
     MGX_SET_LDS(mgx_fixup_kernel, h->lds_refill);
 #undef MGX_SET_LDS
