@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
     ap.add_argument("--probe", type=int, default=256, help="eager steps timed per launch for the roofline")
     ap.add_argument("--workload", default="rollout", choices=["rollout", "ppo"])
+    ap.add_argument("--refill-every", type=int, default=0, help="steps per refill epoch (0 = engine default, D/4)")
+    ap.add_argument("--refill-cap", type=int, default=0, help="extra episodes per env per epoch (0 = engine default)")
+    ap.add_argument("--ring-depth", type=int, default=0, help="episode ring depth (0 = engine default)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
                     help="BASELINE.json config preset (per-GPU share): 2 GTG 8x8 65,536 envs; "
                          "4 ALL mixed 8x8 32,768 envs (256k over 8 GPUs); 5 TGL 16x16 131,072 envs (1M over 8)")
@@ -226,7 +229,8 @@ def main():
     n = args.n_envs
     mission = None if args.mission == "None" else int(args.mission)
     eng = MgxEngine(problem=args.problem, mission=mission, size=args.size, n_envs=n, seed=42,
-                    env_index_offset=rank * n, n_stack=args.n_stack, terminal_mode="truncated", device=dev)
+                    env_index_offset=rank * n, n_stack=args.n_stack, terminal_mode="truncated", device=dev,
+                    refill_every=args.refill_every, refill_cap=args.refill_cap, ring_depth=args.ring_depth)
     K, W = args.steps, args.warmup
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)

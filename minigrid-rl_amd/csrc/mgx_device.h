@@ -221,6 +221,9 @@ __device__ __forceinline__ void pcg_seed(Pcg &p, uint64_t seed) {
 // compare tests ten candidate words at once (see randbelow).
 constexpr int MT_FIELDS = 10;       // words per packed group
 constexpr int MT_WG = 16;           // groups per lane-private LDS window (160 words)
+#ifndef MGX_MT_TOPUP
+#define MGX_MT_TOPUP 4      // window top-up when a lane has fewer than this many groups left (0: off)
+#endif
 constexpr int WIN_STRIDE = 34;      // dwords per lane window row: 8-B aligned, 2-way banked for b64
 constexpr uint64_t MT_REP = 0x041041041041041ull;   // 1 in every 6-bit slot of ten
 constexpr uint64_t MT_LOW60 = (1ull << 60) - 1ull;
@@ -355,6 +358,23 @@ __device__ __forceinline__ uint64_t win_group(Gen<NW> &G, uint64_t g) {
     return G.win[off];
 }
 __device__ __forceinline__ uint64_t div10(uint64_t v) { return __umul64hi(v, 0xCCCCCCCCCCCCCCCDull) >> 3; }
+// Wave-uniform window top-up: once some lane's window is nearly used up, every lane whose
+// window is at least half used reloads it at its current group, together: one load round
+// trip for the wave instead of one per lane at the moment its window runs out (then the
+// whole wave waits on that lane alone).  Same table words, so results are unchanged.
+template <int NW>
+__device__ __forceinline__ void mt_topup(Gen<NW> &G) {
+#if MGX_MT_TOPUP
+    const uint64_t g = div10(G.cur);
+    const int64_t used = (int64_t)(g - G.gbase);              // < 0 right after a look-ahead refill
+    if (__ballot(used >= MT_WG - MGX_MT_TOPUP)) {
+        if (used >= MT_WG / 2 && g + MT_WG <= G.tlen) {
+            GCOUNT(G, 25);
+            G.gbase = mt_refill_cold(G.table, G.tlen, (lds_u64 *)G.win, g);
+        }
+    }
+#endif
+}
 // (re)load the group registers at the current cursor
 template <int NW>
 __device__ __forceinline__ void mt_sync(Gen<NW> &G) {
@@ -749,6 +769,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
 #pragma unroll 1
     while (!fin) {
         GCOUNT(G, 20);
+        mt_topup(G);
         int x0, x1, y0, y1;
         room_rect(nr, r, mid, S, x0, x1, y0, y1);
         const bool is_key = phase < 2;

@@ -19,7 +19,7 @@ names = {8: "copyout+loop", 9: "setup", 10: "mission+nr", 11: "walls+door draws"
 waves = (n + 63) // 64; epochs = 192 // e.refill_every
 res = {names[k]: round((c1[k] - c0[k]) / waves / epochs) for k in names}
 res["total_per_wave_epoch"] = sum(res.values())
-for k, nm in ((20, "room_task_iters"), (21, "randbelow_iters"), (24, "randbelow_calls"), (22, "free_cell_iters"), (23, "mt_refills")):
+for k, nm in ((20, "room_task_iters"), (21, "randbelow_iters"), (24, "randbelow_calls"), (22, "free_cell_iters"), (23, "mt_refills"), (25, "mt_topups")):
     res[nm] = round((c1[k] - c0[k]) / waves / epochs, 1)
 res["episodes_per_wave_epoch"] = (s1["resets"] - s0["resets"]) / waves / epochs
 print(json.dumps(res))
