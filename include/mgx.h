@@ -63,7 +63,7 @@ typedef enum { MGX_TERMINAL_NONE = 0, MGX_TERMINAL_TRUNCATED = 1, MGX_TERMINAL_A
 #define MGX_DEVERR_MT_TABLE   1u   /* an env ran past the MT19937 output table */
 #define MGX_DEVERR_BAD_ACTION 2u   /* action outside 0..6 (minigrid raises ValueError) */
 #define MGX_DEVERR_PCG_LOOP   4u   /* a PCG64 rejection loop exceeded its safety bound */
-#define MGX_DEVERR_OBJECTS    8u   /* generator ran out of objects (AssertionError in the reference) */
+#define MGX_DEVERR_OBJECTS    8u   /* generator ran out of objects (AssertionError / IndexError in the reference) */
 #define MGX_DEVERR_RING_EMPTY 16u  /* an env found its episode ring empty (engine invariant broken) */
 
 typedef struct mgx_config {

@@ -18,7 +18,7 @@ ABI_VERSION = 2        # == MGX_ABI_VERSION (include/mgx.h)
 PROBLEMS = {"multi": 0, "full": 1, "gto": 2, "gtg": 3, "opn": 4, "pkp": 5, "drp": 6, "mov": 7}
 TERMINAL = {"none": 0, "truncated": 1, "all": 2}
 DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unknown action)",
-          4: "PCG64 rejection loop bound exceeded", 8: "object list exhausted (AssertionError)",
+          4: "PCG64 rejection loop bound exceeded", 8: "object list exhausted (AssertionError / IndexError in the reference)",
           16: "episode ring ran dry (engine invariant broken)"}
 
 # Every entry point include/mgx.h declares (checked by tests/test_abi.py).

@@ -269,6 +269,9 @@ CONFIGS += [
     ("novis_single_gto_s11", dict(problem="gto", mission=None, size=11, see_through_walls=False, num_objects=12)),
     ("novis_obst_multi_tgl_s16", dict(problem="multi", mission=1, size=16, see_through_walls=False,
                                       obstacles=True, percent_obstacles=0.1)),
+    # crowded rooms (8 objects; the reference itself raises IndexError once locked doors have
+    # taken enough of the 18 (type, colour) choices, e.g. at 18 objects)
+    ("multi_all_s11_o8", dict(problem="multi", mission=None, size=11, num_objects=8)),
 ]
 
 

@@ -183,6 +183,55 @@ def test_engine_matches_oracle_1024_envs(problem, mission, size):
     eng.poll_error()
 
 
+@pytest.mark.parametrize("problem,mission,size,nobj", [("multi", None, 8, 8), ("multi", None, 11, 8),
+                                                       ("full", None, 8, 0), ("gtg", None, 8, 24)])
+def test_engine_matches_oracle_object_capacity(problem, mission, size, nobj):
+    """The generator's per-lane object list is sized per config (mgx_create: obj_cap).  At large
+    object counts (single room: the most the 8x8 room holds; multi: crowded rooms, pinned by the
+    multi_all_s11_o8 reference fixture) transitions stay bit-exact vs the C oracle and no error bit
+    is raised (512 envs x 128 random steps)."""
+    _need_gpu()
+    import oracle as O
+    from mgx import MgxEngine
+    n, T = 512, 128
+    ov = O.OracleVec(problem, mission, size, nobj, n, 42)
+    eng = MgxEngine(problem=problem, mission=mission, size=size, num_objects=nobj, n_envs=n, n_stack=4,
+                    terminal_mode="all", reward64=True)
+    r = ov.reset()
+    obs = eng.reset()
+    img, dr, mi = EngineSource.newest(obs)
+    assert np.array_equal(img, r["image"]) and np.array_equal(mi, r["mission"])
+    acts = np.random.default_rng(7).integers(0, 7, (T, n))
+    for t in range(T):
+        o = ov.step(acts[t])
+        obs = eng.step(torch.as_tensor(acts[t], device=eng.device))
+        done = eng.done.cpu().numpy().astype(bool)
+        assert np.array_equal(done, (o["terminated"] | o["truncated"]).astype(bool)), t
+        assert np.array_equal(eng.reward64.cpu().numpy(), o["reward"]), t
+        img, dr, mi = EngineSource.newest(obs)
+        timg, tdr, tmi = EngineSource.newest(eng.terminal_obs)
+        assert np.array_equal(np.where(done[:, None, None, None], timg, img), o["image"]), t
+        assert np.array_equal(np.where(done[:, None], tmi, mi), o["mission"]), t
+    a, b = eng.dump_state(), ov.dump()
+    for k in ("grid", "agent", "mtwords", "pcg", "target"):
+        assert np.array_equal(a[k], b[k]), k
+    eng.poll_error()
+
+
+def test_objects_exhausted_is_reported():
+    """multi with 18 objects: once locked doors have taken their keys (and key boxes) out of the 18
+    (type, colour) choices, the reference's `choice(obj_choice)` raises IndexError
+    (custom_env.py:1236).  The engine must report it (MGX_DEVERR_OBJECTS), never go on silently."""
+    _need_gpu()
+    from mgx import MgxEngine, MgxError
+    eng = MgxEngine(problem="multi", mission=None, size=11, num_objects=18, n_envs=512)
+    eng.reset()
+    with pytest.raises(MgxError, match="object list exhausted"):
+        for _ in range(64):
+            eng.step(torch.full((512,), 6, dtype=torch.int32, device=eng.device))   # 'done': reset every step
+        eng.poll_error()
+
+
 def test_gae_bit_exact():
     _need_gpu()
     import oracle as O
