@@ -47,8 +47,8 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2048)
-    ap.add_argument("--warmup", type=int, default=128)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (rollout 2048; ppo: PPO iterations, 4)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (rollout 128; ppo: 1)")
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--problem", default="multi")
     ap.add_argument("--mission", default="5")
@@ -73,6 +73,11 @@ def parse():
     for k, v in presets[args.config].items():          # a preset fills what was not given explicitly
         if getattr(args, k) == ap.get_default(k):
             setattr(args, k, v)
+    ppo = args.workload == "ppo"
+    if args.steps is None:
+        args.steps = 4 if ppo else 2048
+    if args.warmup is None:
+        args.warmup = 1 if ppo else 128
     return args
 
 
@@ -166,17 +171,21 @@ def main_ppo(args, world, rank, local, dev):
         torch.cuda.synchronize(dev)
         return t1 - t0, time.perf_counter() - t1
 
-    for _ in range(W):
-        iteration()
+    for i in range(W):
+        a, b = iteration()
+        if rank == 0:
+            print("ppo warmup %d: collect %.3fs train %.3fs" % (i, a, b), file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     tc = tt = 0.0
-    for _ in range(K):
+    for i in range(K):
         a, b = iteration()
         tc += a
         tt += b
+        if rank == 0:
+            print("ppo iter %d: collect %.3fs train %.3fs" % (i, a, b), file=sys.stderr, flush=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
