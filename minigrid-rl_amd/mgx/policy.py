@@ -81,7 +81,7 @@ class CustomExtractor(nn.Module):
         self.n_frames_stack = n_frames_stack
         self.mission_cache = mission_cache
         self.gru_chunk = 16384          # MIOpen's RNN rejects very large batches (miopenStatusBadParm)
-        self.aten_gru = False
+        self.aten_gru = os.environ.get("MGX_ATEN_GRU", "0") == "1"
         self.gru = False
         ext = {}
         total = 0
