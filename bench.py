@@ -8,6 +8,12 @@ VecFrameStack(4) roll + SubprocVecEnv auto-reset, i.e. one `mgx_step`):
   warmup+timed steps, so inputs are resident in HBM), seed 42, env global
   index i seeded 42+i (rank r owns [r*N, (r+1)*N)) -> weak scaling.
 
+The timed region pays for every reset it consumes: it is a whole number of
+refill epochs (the episode generator's launches are inside it; `window` reports
+episodes produced vs consumed), and every `horizon` steps it runs GAE over the
+rewards/dones the steps wrote (mgx_gae_dones, synthetic values) and, for N>1,
+the one all-reduce of the (sum A, sum A^2, n) advantage statistics (RCCL).
+
 Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel
 (mgx_step_kernel) with SURVEY.md §8(d)'s algorithmic bytes
   B_alg = 334*steps + (3*S^2 + 208)*resets     (per launch: one step of all N envs)
@@ -15,8 +21,9 @@ divided by its average launch duration, measured live with HIP events on the
 launch stream around each run of consecutive mgx_step calls that neither fork nor join a refill epoch
 (so the event pair brackets only mgx_step_kernel launches, which still run
 concurrently with that epoch's refill, as in the timed region);
-`traffic` is the rocprofv3 PMC figure committed under profiles/.
-`cpu_baseline` times the C oracle (oracle/, single thread) on a bounded sample.
+`traffic` is the rocprofv3 PMC figure committed under profiles/.  `gae` times
+mgx_gae_dones alone at the horizon and at T=1024 (17 B per element).
+`cpu_baseline` times the C port of the env (oracle/) on this host's cores.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
@@ -64,7 +71,9 @@ def parse():
     ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
                     help="BASELINE.json config preset (per-GPU share): 2 GTG 8x8 65,536 envs; "
                          "4 ALL mixed 8x8 32,768 envs (256k over 8 GPUs); 5 TGL 16x16 131,072 envs (1M over 8)")
-    ap.add_argument("--horizon", type=int, default=16, help="ppo: env steps per rollout")
+    ap.add_argument("--horizon", type=int, default=None,
+                    help="env steps per rollout (rollout: GAE + adv-stat reduction cadence, default the "
+                         "largest whole-epoch divisor of --steps up to 1024; ppo: default 16)")
     ap.add_argument("--batch-size", type=int, default=65536, help="ppo: minibatch size")
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
     args = ap.parse_args()
@@ -78,30 +87,62 @@ def parse():
         args.steps = 4 if ppo else 2048
     if args.warmup is None:
         args.warmup = 1 if ppo else 128
+    if ppo and args.horizon is None:
+        args.horizon = 16
     return args
 
 
-def cpu_baseline(args, seconds):
-    """C oracle (oracle/libmgx_oracle.so), one thread, same config, bounded sample."""
-    import numpy as np
+def _cpu_leg(problem, mission, size, n, seconds, seed, q=None):
+    """One CPU-baseline process: the C port (oracle/mgx_oracle.c, orc_bench) stepping `n` envs
+    with random actions for about `seconds`; returns (env_steps, seconds)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    n = 1024
-    mission = None if args.mission == "None" else int(args.mission)
-    v = O.OracleVec(args.problem, mission, args.size, 4, n, 42)
+    v = O.OracleVec(problem, mission, size, 4, n, 42)
     v.reset()
-    rng = np.random.default_rng(1234)
-    steps = 0
+    steps = max(1, 20000 // n)
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        acts = rng.integers(0, 7, (16, n)).astype(np.int32)
-        for k in range(16):
-            v.step(acts[k])
-        steps += 16
+    v.bench(steps, seed)                                   # calibration run (counted)
+    done = steps
     dt = time.perf_counter() - t0
-    return dict(value=n * steps / dt, unit="env-steps/s", cores=1, kind="port",
-                sample="C oracle (oracle/mgx_oracle.c), 1 thread, %d envs x %d steps (%.1fs), same config, "
-                       "auto-reset included; host: %s" % (n, steps, dt, _cpu_model()))
+    steps = max(1, int(done * (seconds - dt) / max(dt, 1e-6)))
+    v.bench(steps, seed + 1)
+    done += steps
+    out = (n * done, time.perf_counter() - t0)
+    if q is not None:
+        q.put(out)
+    return out
+
+
+def cpu_baseline(args, seconds):
+    """SURVEY.md 8(d) CPU baseline, timed on this host BEFORE the GPU is touched: the C port of
+    the reference-shaped env (oracle/, object grid + literal slice/rotate/encode per step,
+    random actions, auto-reset) in three legs of about `seconds` each:
+      all-cores  P processes, one env each (the SubprocVecEnv analogue, ppo.py:121),
+                 P = this process's CPU share (affinity, at most 16 on a shared GPU box);
+      1 thread   1 process stepping 1,024 envs of the same config;
+      config 1   1 process, 1 env, GTG 8x8 (BASELINE configs[0])."""
+    import multiprocessing as mp
+    mission = None if args.mission == "None" else int(args.mission)
+    P = max(1, min(len(os.sched_getaffinity(0)), 16))
+    ctx = mp.get_context("fork")                           # no GPU state exists yet in this process
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cpu_leg, args=(args.problem, mission, args.size, 1, seconds, 7 + i, q))
+             for i in range(P)]
+    for pr in procs:
+        pr.start()
+    res = [q.get() for _ in procs]
+    for pr in procs:
+        pr.join()
+    all_cores = sum(r[0] for r in res) / max(r[1] for r in res)
+    s1, t1 = _cpu_leg(args.problem, mission, args.size, 1024, seconds, 3)
+    c1, tc1 = _cpu_leg("multi", 5, 8, 1, seconds, 5)
+    return dict(value=all_cores, unit="env-steps/s", cores=P, kind="port",
+                sample="C port of the reference env (oracle/mgx_oracle.c orc_bench: object grid, slice+rotate+"
+                       "encode per step, tokenised mission, auto-reset), random actions, same config as the GPU "
+                       "line; %d processes x 1 env x %.1fs; host: %s" % (P, seconds, _cpu_model()),
+                legs={"all_cores": {"value": all_cores, "processes": P, "envs_per_process": 1},
+                      "one_thread": {"value": s1 / t1, "processes": 1, "envs": 1024, "seconds": t1},
+                      "config1_gtg8_1env": {"value": c1 / tc1, "processes": 1, "envs": 1, "seconds": tc1}})
 
 
 def _workload_name(args, mission, n, world):
@@ -213,11 +254,64 @@ def main_ppo(args, world, rank, local, dev):
         dist.destroy_process_group()
 
 
+def pick_epoch(K, D=128):
+    """Refill epoch E (mgx refill_every) so that the K timed steps are whole epochs: the largest
+    divisor of K in [8, D/2] (a ring must hold 2E episodes); K < 8 -> E = K.  None when K has no
+    such divisor (then E = D/4 and the timed region ends with mgx_join, paying for the whole
+    last epoch's refill)."""
+    for E in range(min(64, D // 2), 7, -1):
+        if K % E == 0:
+            return E
+    return K if K < 8 else None
+
+
+def pick_horizon(K, E, req):
+    """Rollout horizon H (GAE + advantage-stat all-reduce every H steps): a multiple of E that
+    divides K, at most 1,024 (algorithm/ppo.yaml:30 n_steps); `req` if it qualifies."""
+    if req and K % req == 0 and (E is None or req % E == 0):
+        return req
+    best = None
+    for H in range(1, min(K, 1024) + 1):
+        if K % H == 0 and (E is None or H % E == 0):
+            best = H
+    return best or K
+
+
+def gae_probe(dev, n, T, reps=20):
+    """Average duration of mgx_gae_dones over [T, n] (HIP events on the launch stream)."""
+    from mgx import gae_dones
+    g = torch.Generator(device=dev)
+    g.manual_seed(77)
+    r = torch.randn((T, n), device=dev, generator=g)
+    v = torch.randn((T, n), device=dev, generator=g)
+    d = (torch.rand((T, n), device=dev, generator=g) < 0.14).to(torch.uint8)
+    lv = torch.randn(n, device=dev, generator=g)
+    out = (torch.empty_like(r), torch.empty_like(r))
+    st = torch.zeros(3, dtype=torch.float64, device=dev)
+    for _ in range(3):
+        gae_dones(r, v, d, lv, 0.8108071290665859, 0.9452281119742252, stats=st, out=out)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        gae_dones(r, v, d, lv, 0.8108071290665859, 0.9452281119742252, stats=st, out=out)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    b = 17.0 * T * n                                  # SURVEY.md 8(d): r 4 + v 4 + done 1 + adv 4 + ret 4
+    del r, v, d, out
+    return {"T": T, "N": n, "avg_launch_us": us, "alg_bytes": b, "achieved": b / us / 1e3,
+            "frac": b / us / 1e3 / PEAK_HBM_GBPS, "unit": "GB/s"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if args.workload == "rollout" and args.cpu_seconds > 0 and world == 1:
+        cpu = cpu_baseline(args, args.cpu_seconds)      # before any GPU call (forks workers)
     # one process per GPU; `local % device_count` only matters for a rehearsal of the
     # N>1 path with more ranks than GPUs (MGX_DIST_BACKEND=gloo: RCCL refuses shared GPUs)
     ndev = torch.cuda.device_count()
@@ -233,51 +327,81 @@ def main():
     dev = torch.device("cuda", gpu)
     if args.workload == "ppo":
         return main_ppo(args, world, rank, local, dev)
-    from mgx import MgxEngine
+    from mgx import MgxEngine, gae_dones
 
     n = args.n_envs
     mission = None if args.mission == "None" else int(args.mission)
+    K = args.steps
+    D = args.ring_depth or 128
+    E = args.refill_every or pick_epoch(K, D)
+    aligned = E is not None and K % E == 0
     eng = MgxEngine(problem=args.problem, mission=mission, size=args.size, n_envs=n, seed=42,
                     env_index_offset=rank * n, n_stack=args.n_stack, terminal_mode="truncated", device=dev,
-                    refill_every=args.refill_every, refill_cap=args.refill_cap, ring_depth=args.ring_depth)
-    K, W = args.steps, args.warmup
+                    refill_every=E or 0, refill_cap=args.refill_cap, ring_depth=args.ring_depth)
+    E = eng.refill_every
+    H = pick_horizon(K, E if aligned else None, args.horizon or 0)
+    W = -(-args.warmup // E) * E                         # warm-up rounded up to whole refill epochs
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     P = args.probe
     actions = torch.randint(0, 7, (W + K + P, n), device=dev, generator=g, dtype=torch.int32)
+    # rollout storage the steps write directly (compact layout): reward f32 and done u8 per step;
+    # values are synthetic (the rollout bench has no policy); GAE + the (sum A, sum A^2, n)
+    # all-reduce run once per horizon inside the timed region
+    rew = torch.zeros((H, n), dtype=torch.float32, device=dev)
+    dones = torch.zeros((H, n), dtype=torch.uint8, device=dev)
+    vals = torch.randn((H, n), device=dev, generator=g)
+    last_v = torch.randn(n, device=dev, generator=g)
+    adv, ret = torch.empty_like(rew), torch.empty_like(rew)
+    st = torch.zeros(3, dtype=torch.float64, device=dev)
+    gamma, lam = 0.8108071290665859, 0.9452281119742252
     eng.reset()
     stream = torch.cuda.current_stream(dev)
     for t in range(W):
         eng.step(actions[t])
     torch.cuda.synchronize(dev)
-    graph = None
+    assert eng.calls % E == 0                            # the timed region starts on an epoch boundary
+
+    def chunk(c):
+        st.zero_()
+        for j in range(H):
+            eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
+        if not aligned and c == K // H - 1:
+            eng.join()                                   # last epoch still forked: pay for all of it
+        gae_dones(rew, vals, dones, last_v, gamma, lam, stats=st, out=(adv, ret))
+
+    nchunks = K // H
+    graphs = []
     if args.graph:
-        # capture the K timed steps once (launch-bound loop -> one hipGraph replay)
-        graph = torch.cuda.CUDAGraph()
+        # one hipGraph per horizon chunk (launch-bound loop -> one replay each); a chunk is whole
+        # refill epochs, so each graph holds its forks and joins (self-contained capture)
         s = torch.cuda.Stream(dev)
         with torch.cuda.stream(s):
-            graph.capture_begin()
-            for t in range(K):
-                eng.step(actions[W + t])
-            eng.join()                      # capture must not end with the refill still forked
-            graph.capture_end()
+            for c in range(nchunks):
+                gr = torch.cuda.CUDAGraph()
+                gr.capture_begin()
+                chunk(c)
+                gr.capture_end()
+                graphs.append(gr)
         torch.cuda.synchronize(dev)
     st0 = eng.stats()
+    hist = torch.zeros((nchunks, 3), dtype=torch.float64, device=dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    if graph is not None:
-        ev0.record(stream)
-        graph.replay()
-        ev1.record(stream)
-    else:
-        ev0.record(stream)
-        for t in range(K):
-            eng.step(actions[W + t])
-        ev1.record(stream)
+    ev0.record(stream)
+    for c in range(nchunks):
+        if graphs:
+            graphs[c].replay()
+        else:
+            chunk(c)
+        hist[c].copy_(st)
+        if world > 1:                                    # the one exchange per rollout
+            hist[c].copy_(_allreduce(hist[c], dist.ReduceOp.SUM))
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -320,6 +444,10 @@ def main():
     wall_max, gpu_max = float(elapsed[0]), float(elapsed[1])
     total_env_steps, total_resets = float(steps_done[0]), float(steps_done[1])
     assert int(total_env_steps) == n * K * world, (total_env_steps, n * K * world)
+    hs = hist.cpu().numpy()
+    assert abs(hs[:, 2].sum() - float(H) * n * world * nchunks) < 0.5, hs    # every chunk's GAE ran
+    gae_h = gae_probe(dev, n, H)
+    gae_1k = gae_probe(dev, n, 1024) if H != 1024 else gae_h
     if rank == 0:
         per_launch_s = (sum(probe_us) / len(probe_us)) * 1e-6 if probe_us else float(gpu_ms) / 1e3 / K
         resets_per_launch = (st1["resets"] - st0["resets"]) / K
@@ -346,11 +474,19 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (uniform random actions on {0..6}, seed 1234+rank; env i seeded 42+i)",
+            "data": "synthetic (uniform random actions on {0..6}, seed 1234+rank; env i seeded 42+i; "
+                    "synthetic values for GAE)",
             "config": {"workload": _workload_name(args, mission, n, world),
                        "problem": args.problem, "mission": mission, "size": args.size, "num_objects": 4,
                        "envs_per_gpu": n, "n_stack": args.n_stack, "parallelism": "env-sharded dp%d" % world,
-                       "hipgraph": bool(graph is not None)},
+                       "hipgraph": bool(graphs), "refill_every": E, "horizon": H,
+                       "timed": "%d steps = %d whole refill epochs%s; GAE + adv-stat %s every %d steps" % (
+                           K, K // E, "" if aligned else " + a joined partial one",
+                           "all-reduce (%s)" % dist.get_backend() if world > 1 else "accumulation", H)},
+            "window": {"refill_launches": st1["refill_launches"] - st0["refill_launches"],
+                       "episodes_produced": (st1["resets"] - st0["resets"]) + (st1["queued"] - st0["queued"]),
+                       "episodes_consumed": st1["resets"] - st0["resets"],
+                       "gae_launches": nchunks},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
                          "kernel": "mgx_step_kernel", "avg_launch_us": per_launch_s * 1e6,
@@ -359,10 +495,11 @@ def main():
                          "alg_bytes_per_launch": b_alg, "resets_per_launch": resets_per_launch,
                          "stack_bytes_per_launch": stack_bytes,
                          "achieved_incl_stack": (b_alg + stack_bytes) / per_launch_s / 1e9},
+            "gae": {"horizon": gae_h, "T1024": gae_1k},
             "gpu_time_ms": gpu_max * 1e3,
         }
-        if args.cpu_seconds > 0 and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

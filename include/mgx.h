@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MGX_ABI_VERSION 2
+#define MGX_ABI_VERSION 3
 
 /* Live-lock cap (engine policy; the reference hangs): a
  * reset attempt may consume at most this many MT19937 words; the attempt that
@@ -164,13 +164,23 @@ mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const floa
                    float gamma, float gamma_lambda, float *advantages_dev, float *returns_dev,
                    double *adv_stats_dev, void *stream);
 
+/* GAE over the compact rollout layout: dones_dev u8 [T][N] is the `done` output of
+ * step t (what mgx_step writes to done_dev), so next_non_terminal(t) = 1 - dones[t]
+ * -- SB3's episode_starts[t+1] for t < T-1 and its last_dones at T-1.  Same fp32
+ * op order, outputs and adv_stats_dev as mgx_gae; 17 B of traffic per element. */
+mgx_status mgx_gae_dones(const float *rewards_dev, const float *values_dev, const uint8_t *dones_dev,
+                         const float *last_values_dev, int64_t T, int64_t N, float gamma, float gamma_lambda,
+                         float *advantages_dev, float *returns_dev, double *adv_stats_dev, void *stream);
+
 /* Synchronises `stream`, returns the device error bits (MGX_DEVERR_*) and clears them. */
 mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits);
 
 /* Counters since create: [0] env-steps, [1] resets (incl. first), [2] abandoned
- * (live-locked) reset attempts, [3] max MT cursor, [4..7] per-phase shader-clock
- * sums of mgx_step_kernel (non-zero only in a -DMGX_STAMPS diagnostic build).
- * Synchronises `stream`. */
+ * (live-locked) reset attempts, [3] max MT cursor, [4] pre-generated episodes
+ * queued in the rings now (between two mgx_reset calls, episodes produced by
+ * the refill = resets consumed + change of [4]), [5] refill launches enqueued (incl. the
+ * synchronous fills of mgx_reset), [6] mgx_step calls since the last mgx_reset,
+ * [7] reserved (0).  Synchronises `stream` and the refill stream. */
 mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]);
 
 /* Diagnostics: the first n (<= 32) raw device counters (phase / section clocks of

@@ -1141,8 +1141,40 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
 // ================================================================ GAE kernel
 // DictRolloutBuffer.compute_returns_and_advantage (SB3; fp32, numpy op order,
 // built with -ffp-contract=off):  delta = ((r + (g*nv)*nnt) - V);  last = delta + (c*nnt)*last
+// The recurrence is serial in t and must round exactly like the sequential numpy loop, so
+// the only parallelism is one column (env) per lane.  Latency, not bandwidth, bounds a
+// naive walk (one dependent load round trip per t): the loads of the next GAE_U steps are
+// issued before the current GAE_U are computed (register double buffer), so each lane keeps
+// 3*GAE_U loads in flight.  DONES: the compact form -- `es` is u8 dones[T][N] (done after
+// step t), next_non_terminal(t) = 1 - dones[t]; otherwise SB3's f32 episode_starts[T][N]
+// plus last_dones (next_non_terminal(t) = 1 - episode_starts[t+1], 1 - last_dones at T-1).
+constexpr int GAE_U = 8;
+
+template <bool DONES>
+struct GaeChunk {
+    float r[GAE_U], v[GAE_U], e[GAE_U];
+};
+
+template <bool DONES>
+__device__ __forceinline__ void gae_load(GaeChunk<DONES> &c, const float *__restrict__ r, const float *__restrict__ v,
+                                         const void *__restrict__ es, int64_t t, int64_t N, int64_t i) {
+    // chunk = steps t, t-1, ..., t-GAE_U+1 (entries with t-j < 0 are never used).  For the f32
+    // form the flag loaded for step t-j is episode_starts[t-j] (used by step t-j-1).
+#pragma unroll
+    for (int j = 0; j < GAE_U; j++) {
+        const int64_t tt = t - j;
+        if (tt >= 0) {
+            const int64_t k = tt * N + i;
+            c.r[j] = r[k];
+            c.v[j] = v[k];
+            c.e[j] = DONES ? (float)static_cast<const uint8_t *>(es)[k] : static_cast<const float *>(es)[k];
+        }
+    }
+}
+
+template <bool DONES>
 __global__ __launch_bounds__(256) void mgx_gae_kernel(const float *__restrict__ r, const float *__restrict__ v,
-                                                      const float *__restrict__ es, const float *__restrict__ lv,
+                                                      const void *__restrict__ es, const float *__restrict__ lv,
                                                       const uint8_t *__restrict__ ld, int64_t T, int64_t N, float g,
                                                       float c, float *__restrict__ adv, float *__restrict__ ret,
                                                       double *__restrict__ stats) {
@@ -1150,21 +1182,30 @@ __global__ __launch_bounds__(256) void mgx_gae_kernel(const float *__restrict__ 
     double s1 = 0.0, s2 = 0.0;
     if (i < N) {
         float last = 0.0f;
-        float nnt = 1.0f - (float)ld[i];
+        float nnt = DONES ? 0.0f : 1.0f - (float)ld[i];     // DONES: set from dones[t] per step
         float nv = lv[i];
-        for (int64_t t = T - 1; t >= 0; --t) {
-            const int64_t k = t * N + i;
-            const float vt = v[k];
-            const float rt = r[k];
-            const float est = es[k];
-            const float delta = (rt + (g * nv) * nnt) - vt;
-            last = delta + (c * nnt) * last;
-            adv[k] = last;
-            ret[k] = last + vt;
-            s1 += (double)last;
-            s2 += (double)last * (double)last;
-            nnt = 1.0f - est;       // for step t-1: 1 - episode_starts[t]
-            nv = vt;
+        GaeChunk<DONES> cur, nxt;
+        gae_load(cur, r, v, es, T - 1, N, i);
+        for (int64_t t0 = T - 1; t0 >= 0; t0 -= GAE_U) {
+            if (t0 - GAE_U >= 0) gae_load(nxt, r, v, es, t0 - GAE_U, N, i);
+#pragma unroll
+            for (int j = 0; j < GAE_U; j++) {
+                const int64_t t = t0 - j;
+                if (t >= 0) {
+                    const int64_t k = t * N + i;
+                    if (DONES) nnt = 1.0f - cur.e[j];
+                    const float vt = cur.v[j];
+                    const float delta = (cur.r[j] + (g * nv) * nnt) - vt;
+                    last = delta + (c * nnt) * last;
+                    adv[k] = last;
+                    ret[k] = last + vt;
+                    s1 += (double)last;
+                    s2 += (double)last * (double)last;
+                    if (!DONES) nnt = 1.0f - cur.e[j];   // for step t-1: 1 - episode_starts[t]
+                    nv = vt;
+                }
+            }
+            cur = nxt;
         }
     }
     if (stats) {
@@ -1301,6 +1342,7 @@ struct mgx_handle {
     int refill_every;       // K: steps per refill epoch
     uint64_t calls;         // mgx_step calls since the last mgx_reset
     uint64_t resets;        // mgx_reset calls since create
+    uint64_t refill_launches;  // refill kernels enqueued since create (incl. the synchronous initial fills)
     bool seed_pending;      // mgx_set_seed called since the last reset
     bool in_flight;         // a refill forked and not yet joined
     bool serial_refill;     // diagnostics (env MGX_SERIAL_REFILL=1): refill on the caller's stream
@@ -1602,6 +1644,7 @@ mgx_status mgx_destroy(mgx_handle *h) {
 
 static mgx_status launch_refill(mgx_handle *h, void *stream) {
     if (h->kp.D == 0) return MGX_OK;
+    h->refill_launches++;
     const int64_t nblk = (h->kp.n + 63) / 64;
     MGX_GEN_LAUNCH(mgx_refill_kernel, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp);
     HIP_TRY(hipGetLastError());
@@ -1743,9 +1786,23 @@ mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const floa
         !advantages_dev || !returns_dev || T <= 0 || N <= 0)
         return fail(MGX_ERR_INVALID, "mgx_gae: bad argument");
     const int64_t nblk = (N + 255) / 256;
-    hipLaunchKernelGGL(mgx_gae_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, rewards_dev,
-                       values_dev, episode_starts_dev, last_values_dev, last_dones_dev, T, N, gamma, gamma_lambda,
-                       advantages_dev, returns_dev, adv_stats_dev);
+    hipLaunchKernelGGL(mgx_gae_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, rewards_dev,
+                       values_dev, (const void *)episode_starts_dev, last_values_dev, last_dones_dev, T, N, gamma,
+                       gamma_lambda, advantages_dev, returns_dev, adv_stats_dev);
+    HIP_TRY(hipGetLastError());
+    return MGX_OK;
+}
+
+mgx_status mgx_gae_dones(const float *rewards_dev, const float *values_dev, const uint8_t *dones_dev,
+                         const float *last_values_dev, int64_t T, int64_t N, float gamma, float gamma_lambda,
+                         float *advantages_dev, float *returns_dev, double *adv_stats_dev, void *stream) {
+    if (!rewards_dev || !values_dev || !dones_dev || !last_values_dev || !advantages_dev || !returns_dev || T <= 0 ||
+        N <= 0)
+        return fail(MGX_ERR_INVALID, "mgx_gae_dones: bad argument");
+    const int64_t nblk = (N + 255) / 256;
+    hipLaunchKernelGGL(mgx_gae_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, rewards_dev,
+                       values_dev, (const void *)dones_dev, last_values_dev, (const uint8_t *)nullptr, T, N, gamma,
+                       gamma_lambda, advantages_dev, returns_dev, adv_stats_dev);
     HIP_TRY(hipGetLastError());
     return MGX_OK;
 }
@@ -1759,16 +1816,23 @@ mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits) {
     return MGX_OK;
 }
 
-mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[4]) {
+mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]) {
     if (!h || !out) return fail(MGX_ERR_INVALID, "null argument");
     HIP_TRY(hipStreamSynchronize(h->side));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    unsigned long long c[8];
-    HIP_TRY(hipMemcpy(c, h->kp.counters, sizeof c, hipMemcpyDeviceToHost));
     std::vector<ulonglong4> b((size_t)3 * h->kp.nblk);
     HIP_TRY(hipMemcpy(b.data(), h->kp.blk, b.size() * sizeof(ulonglong4), hipMemcpyDeviceToHost));
-    c[0] = c[1] = c[2] = c[3] = 0;
+    uint64_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // blk sections: [0, nblk) step kernel (x steps, y resets), [nblk, 2 nblk) fixup, [2 nblk, 3 nblk)
+    // refill; z live-locks and w max MT cursor in every section
     for (const ulonglong4 &v : b) { c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] = v.w > c[3] ? v.w : c[3]; }
+    if (h->kp.D > 0) {   // episodes queued in the rings: sum of (tail - head) mod 256
+        std::vector<uint8_t> ht((size_t)2 * h->kp.n);
+        HIP_TRY(hipMemcpy(ht.data(), h->kp.ring_head, ht.size(), hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < h->kp.n; i++) c[4] += (uint8_t)(ht[(size_t)(h->kp.n + i)] - ht[(size_t)i]);
+    }
+    c[5] = h->refill_launches;
+    c[6] = h->calls;
     for (int i = 0; i < 8; i++) out[i] = c[i];
     return MGX_OK;
 }

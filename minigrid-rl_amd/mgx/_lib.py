@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MGX_LIB_PATH", os.path.join(HERE, "libmgx.so"))   # override: diagnostic builds
 
 MGX_OK = 0
-ABI_VERSION = 2        # == MGX_ABI_VERSION (include/mgx.h)
+ABI_VERSION = 3        # == MGX_ABI_VERSION (include/mgx.h)
 PROBLEMS = {"multi": 0, "full": 1, "gto": 2, "gtg": 3, "opn": 4, "pkp": 5, "drp": 6, "mov": 7}
 TERMINAL = {"none": 0, "truncated": 1, "all": 2}
 DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unknown action)",
@@ -23,7 +23,7 @@ DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unk
 
 # Every entry point include/mgx.h declares (checked by tests/test_abi.py).
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
-           "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text")
+           "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_gae_dones", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text")
 
 
 class MgxConfig(ctypes.Structure):
@@ -80,6 +80,7 @@ def load():
     L.mgx_set_seed.argtypes = [P, I64]
     L.mgx_get_config.argtypes = [P, ctypes.POINTER(MgxConfig)]
     L.mgx_gae.argtypes = [P, P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P]
+    L.mgx_gae_dones.argtypes = [P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P]
     L.mgx_poll_error.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]
     L.mgx_stats.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64)]
     L.mgx_debug_counters.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]

@@ -128,6 +128,27 @@ class MgxEngine:
         self.calls += 1
         return self.obs
 
+    def step_into(self, actions, reward=None, done=None):
+        """step() with the per-step reward (f32 [N]) and done (u8/bool [N]) outputs written to the
+        given device tensors instead of the engine's own -- e.g. row t of a [T, N] rollout buffer,
+        so a captured graph of T steps fills the buffer without copies."""
+        so = self._step_out
+        if reward is not None or done is not None:
+            so = _lib.MgxStepOut.from_buffer_copy(self._step_out)
+            for t, name, dt in ((reward, "reward_dev", (torch.float32,)), (done, "done_dev", (torch.uint8, torch.bool))):
+                if t is None:
+                    continue
+                if t.device != self.device or t.dtype not in dt or t.numel() != self.n or not t.is_contiguous():
+                    raise ValueError("%s output must be a contiguous %s [%d] tensor on %s" % (name, dt, self.n, self.device))
+                setattr(so, name, t.data_ptr())
+        if actions.device != self.device or actions.dtype not in (torch.int32, torch.int64) \
+                or actions.shape != (self.n,) or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous int32/int64 [%d] tensor on %s" % (self.n, self.device))
+        _lib.check(self.L.mgx_step(self.h, _ptr(actions), actions.element_size(), ctypes.byref(so), self._stream()),
+                   "mgx_step")
+        self.calls += 1
+        return self.obs
+
     def epoch_boundary(self, call=None):
         """True if step call number `call` (default: the next one) forks or joins a refill."""
         c = self.calls if call is None else call
@@ -149,7 +170,7 @@ class MgxEngine:
         out = (ctypes.c_uint64 * 8)()
         _lib.check(self.L.mgx_stats(self.h, self._stream(), out), "mgx_stats")
         return dict(steps=int(out[0]), resets=int(out[1]), livelocks=int(out[2]), max_mt_cursor=int(out[3]),
-                    phase_clocks=[int(out[i]) for i in range(4, 8)])
+                    queued=int(out[4]), refill_launches=int(out[5]), calls=int(out[6]))
 
     def debug_counters(self, n=32):
         """Raw diagnostic counters (section clocks of the stamp builds)."""
@@ -202,4 +223,22 @@ def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lam
     _lib.check(L.mgx_gae(_ptr(rewards), _ptr(values), _ptr(episode_starts), _ptr(lv), _ptr(ld), T, N,
                          ctypes.c_float(gamma), ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats), stream),
                "mgx_gae")
+    return adv, ret
+
+
+def gae_dones(rewards, values, dones, last_values, gamma, gae_lambda, stats=None, out=None):
+    """GAE over the compact rollout layout (libmgx mgx_gae_dones): dones u8/bool [T, N] is
+    the `done` of step t, i.e. SB3's episode_starts shifted by one plus last_dones.
+    Returns (advantages, returns) f32 [T, N] (written into `out` if given)."""
+    L = _lib.load()
+    T, N = rewards.shape
+    for t in (rewards, values):
+        assert t.dtype == torch.float32 and t.is_contiguous() and t.shape == (T, N)
+    assert dones.shape == (T, N) and dones.is_contiguous() and dones.element_size() == 1
+    lv = last_values.reshape(N).float().contiguous()
+    adv, ret = out if out is not None else (torch.empty_like(rewards), torch.empty_like(rewards))
+    gl = float(torch.tensor(gamma * gae_lambda, dtype=torch.float64).float())
+    stream = ctypes.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
+    _lib.check(L.mgx_gae_dones(_ptr(rewards), _ptr(values), _ptr(dones), _ptr(lv), T, N, ctypes.c_float(gamma),
+                               ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats), stream), "mgx_gae_dones")
     return adv, ret

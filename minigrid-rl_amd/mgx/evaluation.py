@@ -87,8 +87,9 @@ class EvalCallback:
     (SB3's documented usage) so the training rollout is not disturbed."""
 
     def __init__(self, eval_engine, best_model_save_path=None, eval_freq=10000, n_eval_episodes=5,
-                 deterministic=True, log=None):
+                 deterministic=True, log=None, callback_on_new_best=None):
         self.eval_engine = eval_engine
+        self.callback_on_new_best = callback_on_new_best   # SB3: its on_step() False stops training
         self.best_model_save_path = best_model_save_path
         self.eval_freq = int(eval_freq)
         self.n_eval_episodes = int(n_eval_episodes)
@@ -119,4 +120,17 @@ class EvalCallback:
             if self.best_model_save_path is not None:
                 os.makedirs(self.best_model_save_path, exist_ok=True)
                 torch.save(policy.state_dict(), os.path.join(self.best_model_save_path, "best_model.pt"))
+            if self.callback_on_new_best is not None:
+                return bool(self.callback_on_new_best.on_step(self))
         return True
+
+
+class StopTrainingOnRewardThreshold:
+    """SB3 StopTrainingOnRewardThreshold, used as EvalCallback(callback_on_new_best=...):
+    training stops once the best mean evaluation reward reaches `reward_threshold`."""
+
+    def __init__(self, reward_threshold):
+        self.reward_threshold = float(reward_threshold)
+
+    def on_step(self, parent):
+        return bool(parent.best_mean_reward < self.reward_threshold)

@@ -74,21 +74,6 @@ def _pack_rows(tok):
     return (t << sh).sum(-1)
 
 
-class _MissionGRU(nn.Module):
-    """Embedding -> GRU -> last hidden state of layer -1, as one module to graph-capture
-    (shares `seq`'s parameters; kept out of the extractor's registered submodules)."""
-
-    def __init__(self, seq, aten_gru):
-        super().__init__()
-        self.seq = seq
-        self.aten_gru = aten_gru
-
-    def forward(self, tok):
-        with torch.backends.cudnn.flags(enabled=not self.aten_gru):
-            _, h = self.seq(tok)
-        return h[-1]
-
-
 class CustomExtractor(nn.Module):
     def __init__(self, obs_shapes, arch=None, n_frames_stack=4, mission_cache=False):
         super().__init__()
@@ -97,17 +82,6 @@ class CustomExtractor(nn.Module):
         self.mission_cache = mission_cache
         self.gru_chunk = 16384          # MIOpen's RNN rejects very large batches (miopenStatusBadParm)
         self.aten_gru = os.environ.get("MGX_ATEN_GRU", "0") == "1"
-        # gru_graph: capture the mission GRU's forward and backward as HIP graphs, one pair per
-        # batch shape (torch.cuda.make_graphed_callables); the update is launch-bound
-        # (measured: 17.1 -> 14.9 ms per 65,536-row minibatch forward+backward, gradients equal to
-        # 1.4e-6 relative; tools/gru_graph_check.py).  One graph's saved activations serve one
-        # backward at a time: a second forward of the same shape before the first one's gradient
-        # has arrived runs eagerly instead (`_pending`).  Off by default: with it on,
-        # tests/test_evaluation.py::test_learn_with_callback_and_final_evaluation hit a HIP
-        # illegal-address fault (error 700) on MI355X; cause not yet found.
-        self.gru_graph = os.environ.get("MGX_GRU_GRAPH", "0") == "1"
-        self.__dict__["_graphed"] = {}   # shape -> graphed callable (not a registered submodule)
-        self.__dict__["_pending"] = set()
         self.gru = False
         ext = {}
         total = 0
@@ -137,18 +111,6 @@ class CustomExtractor(nn.Module):
             return seq(torch.zeros((1,) + tuple(shape))).reshape(1, -1).shape[-1]
 
     def _mission(self, seq, tok):
-        if self.gru and self.gru_graph and tok.is_cuda and torch.is_grad_enabled():
-            key = tuple(tok.shape)
-            if key not in self._pending:
-                fn = self._graphed.get(key)
-                if fn is None:
-                    fn = torch.cuda.make_graphed_callables(_MissionGRU(seq, self.aten_gru), (tok.clone(),))
-                    self._graphed[key] = fn
-                out = fn(tok)
-                if out.requires_grad:
-                    self._pending.add(key)
-                    out.register_hook(lambda g, k=key: self._pending.discard(k))
-                return out
         if self.gru:
             # aten_gru: ATen's per-step fused cell instead of MIOpen's RNN (measured slower
             # on MI355X at these shapes; kept as a switch)

@@ -127,6 +127,7 @@ class RolloutCollector:
         self.last_dones = torch.zeros(engine.n, dtype=torch.bool, device=engine.device)
         self.num_timesteps = 0
         self.ep_returns, self.ep_lens = [], []
+        self.stopped = False           # a callback's on_step returned False (SB3 early stop)
 
     def start(self):
         self.engine.reset()
@@ -163,7 +164,10 @@ class RolloutCollector:
             ep_r.append(torch.where(d, e.ep_return, torch.nan))
             ep_l.append(torch.where(d, e.ep_len.float(), torch.nan))
             if callback is not None:       # BaseCallback.on_step, once per vectorised step
-                callback.on_step(pol, self.num_timesteps)
+                if callback.on_step(pol, self.num_timesteps) is False:
+                    # SB3 collect_rollouts: return False at once (no GAE); learn() stops
+                    self.stopped = True
+                    return None
                 pol.train(False)
         self.last_dones.copy_(e.done)
         last_values = pol.predict_values(e.obs)
@@ -272,6 +276,8 @@ def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None, cal
     world = tr.world
     while col.num_timesteps * world < total_timesteps:
         buf = col.collect(callback)
+        if buf is None:                # callback asked to stop (SB3: continue_training False)
+            break
         progress = 1.0 - float(col.num_timesteps * world) / float(total_timesteps)
         mean, std, s = tr.global_adv_stats(buf)
         st = tr.train(buf, progress)

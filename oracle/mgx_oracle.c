@@ -1007,6 +1007,36 @@ EXPORT void orc_step(orc_vec *v, const int32_t *actions, uint8_t *img, uint8_t *
     }
 }
 
+/* CPU baseline leg of bench.py (cpu_baseline): `steps` vectorised steps of every env with
+ * uniform random actions on 0..6 (xorshift64*, seeded), auto-reset included, each step's
+ * observation emitted (image HWC, direction, mission tokens) into scratch -- the work of
+ * PlaygroundEnv.step + gen_obs + the two wrappers per env-step, without Python overhead.
+ * Returns the number of auto-resets. */
+uint8_t orc_bench_sink[147 + 1 + 32];      /* emitted obs land here (global: not dead stores) */
+EXPORT int64_t orc_bench(orc_vec *v, int64_t steps, uint64_t seed) {
+    uint64_t x = seed * 0x9E3779B97F4A7C15ULL + 1;
+    uint8_t *img = orc_bench_sink, *dir = orc_bench_sink + 147, *mis = orc_bench_sink + 148;
+    int64_t resets = 0;
+    for (int64_t t = 0; t < steps; t++) {
+        for (int i = 0; i < v->n; i++) {
+            env_t *e = &v->e[i];
+            x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+            const int a = (int)(((x * 0x2545F4914F6CDD1DULL) >> 32) % 7u);
+            uint8_t im[7][7][3];
+            double r; int tm, tr;
+            env_step(e, a, im, &r, &tm, &tr);
+            emit_obs(e, 0, &im[0][0][0], img, dir, mis);
+            if (tm || tr) {
+                env_reset(e, 0, 0);
+                gen_obs(e, im);
+                emit_obs(e, 0, &im[0][0][0], img, dir, mis);
+                resets++;
+            }
+        }
+    }
+    return resets;
+}
+
 /* State dump in the fixture layout (tests/golden/make_golden.py). */
 EXPORT void orc_dump(orc_vec *v, uint8_t *grid /*[n][S][S][4] x-major*/, uint8_t *agent /*[n][3]*/,
                      uint8_t *carrying /*[n][4]*/, int32_t *step_count, uint8_t *mission_done,

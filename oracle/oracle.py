@@ -49,6 +49,8 @@ def lib():
         L.orc_reset_ex.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, P, P, P, P]
         L.orc_step.argtypes = [P] * 12
         L.orc_dump.argtypes = [P] * 10
+        L.orc_bench.argtypes = [P, ctypes.c_int64, ctypes.c_uint64]
+        L.orc_bench.restype = ctypes.c_int64
         L.orc_mission.restype = ctypes.c_char_p
         L.orc_mission.argtypes = [P, ctypes.c_int]
         L.orc_mt_words.argtypes = [ctypes.c_uint64, ctypes.c_int, P]
@@ -111,6 +113,10 @@ class OracleVec:
                         _p(rimg), _p(rd), _p(rm), _p(ll))
         return dict(image=img, dir=d, mission=m, reward=rew, terminated=term, truncated=trunc,
                     r_image=rimg, r_dir=rd, r_mission=rm, livelock=ll)
+
+    def bench(self, steps, seed=1234):
+        """`steps` random-action vectorised steps in C (orc_bench; CPU baseline leg) -> resets."""
+        return int(self.L.orc_bench(self.h, int(steps), int(seed)))
 
     def dump(self):
         n, S = self.n, self.S

@@ -242,7 +242,8 @@ def run_config(name, cfg, n, T, seed_actions=1234):
     d["meta"] = np.array([S, n, T, cfg.seed, -1 if cfg.env.mission is None else cfg.env.mission,
                           cfg.env.num_objects], np.int64)
     d["problem"] = np.array(cfg.env.problem)
-    d["env_flags"] = np.array([int(bool(cfg.env.see_through_walls)), int(bool(cfg.env.obstacles))], np.int64)
+    d["env_flags"] = np.array([int(bool(cfg.env.see_through_walls)), int(bool(cfg.env.obstacles)),
+                               int(bool(cfg.env.all_doors_open))], np.int64)
     d["percent_obstacles"] = np.array(float(cfg.env.percent_obstacles), np.float64)
     names = sorted(missions)
     d["mission_names"] = np.array(names)
@@ -272,6 +273,14 @@ CONFIGS += [
     # crowded rooms (8 objects; the reference itself raises IndexError once locked doors have
     # taken enough of the 18 (type, colour) choices, e.g. at 18 objects)
     ("multi_all_s11_o8", dict(problem="multi", mission=None, size=11, num_objects=8)),
+    # all_doors_open=True (shipped by distilling.yaml:27 and moe.yaml:23): no `locked` draw, an extra
+    # `is_open` draw per door (custom_env.py:637-649, 882-928, 1326-...), open doors see-through /
+    # passable / toggled shut.  2-, 3- and 4-room layouts come from the multi problems' randint(2,4).
+    ("ado_multi_all_s8", dict(problem="multi", mission=None, size=8, all_doors_open=True)),
+    ("ado_multi_all_s11", dict(problem="multi", mission=None, size=11, all_doors_open=True)),
+    ("ado_multi_tgl_s16", dict(problem="multi", mission=1, size=16, all_doors_open=True)),
+    ("ado_multi_gtg_s8", dict(problem="multi", mission=5, size=8, all_doors_open=True)),
+    ("ado_single_opn_s8", dict(problem="opn", mission=None, size=8, all_doors_open=True)),
 ]
 
 

@@ -105,3 +105,22 @@ def test_learn_with_callback_and_final_evaluation():
     pol, hist, eng = learn(cfg, total_timesteps=2 * 256 * 16, callback=cb, evaluate=True)
     assert len(hist) == 2 and len(cb.evaluations) == 4
     assert np.isfinite(hist[-1]["mean_reward"]) and 0.0 <= hist[-1]["mean_reward"] <= 1.0
+
+
+@pytest.mark.gpu
+def test_learn_stops_when_callback_returns_false():
+    """SB3 early stop: EvalCallback(callback_on_new_best=StopTrainingOnRewardThreshold(t)) makes
+    on_step return False at the first evaluation that reaches t; collect_rollouts returns at once
+    and learn() ends (no further rollout or update)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mgx import EvalCallback, MgxEngine, StopTrainingOnRewardThreshold
+    from mgx.ppo import PPOConfig, learn
+    cfg = PPOConfig(n_envs=256, horizon=16, batch_size=1024, n_epochs=1,
+                    env=dict(problem="multi", mission=2, size=8, num_objects=4))
+    ev = MgxEngine(problem="multi", mission=2, size=8, n_envs=32, seed=43, reward64=True, device="cuda:0")
+    cb = EvalCallback(ev, eval_freq=8, n_eval_episodes=10,
+                      callback_on_new_best=StopTrainingOnRewardThreshold(-1.0))   # any reward >= -1 stops
+    pol, hist, eng = learn(cfg, total_timesteps=4 * 256 * 16, callback=cb)
+    assert len(cb.evaluations) == 1          # stopped at the first evaluation (step 8 of rollout 0)
+    assert len(hist) == 0                    # the interrupted rollout is not trained on

@@ -91,7 +91,8 @@ def test_engine_matches_reference_fixture(path):
 
 
 @pytest.mark.parametrize("name", ["multi_all_s8", "multi_gtg_s8", "multi_tgl_s16", "single_pkp_s8",
-                                  "single_full_s8", "obst_single_mov_s11", "novis_obst_multi_tgl_s16"])
+                                  "single_full_s8", "obst_single_mov_s11", "novis_obst_multi_tgl_s16",
+                                  "ado_multi_all_s11"])
 @pytest.mark.parametrize("ring", [(-1, 0), (2, 1), (4, 2), (8, 3)], ids=["inline", "ring2", "ring4", "ring8_every3"])
 def test_engine_reset_paths_match_fixture(name, ring):
     """Same fixtures through the other reset paths: episodes generated inline in
@@ -145,18 +146,20 @@ def test_frame_stack_and_terminal_obs_match_sb3_layer(name, n_stack, mdt):
     src.e.poll_error()
 
 
-@pytest.mark.parametrize("problem,mission,size", [("multi", 5, 8), ("multi", None, 8), ("multi", 2, 8),
-                                                  ("multi", None, 16), ("gto", None, 8)])
-def test_engine_matches_oracle_1024_envs(problem, mission, size):
+@pytest.mark.parametrize("problem,mission,size,ado", [("multi", 5, 8, 0), ("multi", None, 8, 0), ("multi", 2, 8, 0),
+                                                      ("multi", None, 16, 0), ("multi", 1, 16, 0), ("gto", None, 8, 0),
+                                                      ("multi", None, 8, 1), ("multi", 1, 16, 1)])
+def test_engine_matches_oracle_1024_envs(problem, mission, size, ado):
     """Bit-exact transitions vs the C oracle at 1,024 envs x 256 random steps
-    (global env index offset 4096 exercises sharded seeding)."""
+    (global env index offset 4096 exercises sharded seeding).  ado: all_doors_open=True
+    (distilling.yaml:27, moe.yaml:23)."""
     _need_gpu()
     import oracle as O
     from mgx import MgxEngine
     n, T, off = 1024, 256, 4096
-    ov = O.OracleVec(problem, mission, size, 4, n, 42, index_offset=off)
+    ov = O.OracleVec(problem, mission, size, 4, n, 42, index_offset=off, all_doors_open=bool(ado))
     eng = MgxEngine(problem=problem, mission=mission, size=size, n_envs=n, env_index_offset=off, n_stack=4,
-                    terminal_mode="all", reward64=True)
+                    terminal_mode="all", reward64=True, all_doors_open=bool(ado))
     r = ov.reset()
     obs = eng.reset()
     img, dr, mi = EngineSource.newest(obs)
@@ -232,92 +235,107 @@ def test_objects_exhausted_is_reported():
         eng.poll_error()
 
 
-def test_gae_bit_exact():
+@pytest.mark.parametrize("T,N", [(1, 300), (7, 513), (64, 4099), (1024, 1000)])
+def test_gae_bit_exact(T, N):
+    """mgx_gae (SB3 f32 episode_starts + last_dones) and mgx_gae_dones (compact u8 dones of each
+    step) against the numpy GAE: advantages and returns bit-exact; the f64 stats triple
+    (sum A, sum A^2, n) that feeds the cross-rank advantage normalisation."""
     _need_gpu()
     import oracle as O
-    from mgx import gae
-    rng = np.random.default_rng(5)
-    T, N = 64, 4099
+    from mgx import gae, gae_dones
+    rng = np.random.default_rng(5 + T)
     r = rng.standard_normal((T, N)).astype(np.float32)
     v = rng.standard_normal((T, N)).astype(np.float32)
-    es = (rng.random((T, N)) < 0.15).astype(np.float32)
+    dones = rng.random((T, N)) < 0.15
+    es = np.zeros((T, N), np.float32)                 # episode_starts[t] = dones[t-1]
+    es[1:] = dones[:-1]
+    es[0] = rng.random(N) < 0.5
     lv = rng.standard_normal(N).astype(np.float32)
-    ld = rng.random(N) < 0.2
+    ld = dones[-1]
     g, lam = 0.8108071290665859, 0.9452281119742252
     want_a, want_r = O.gae(r, v, es, lv, ld, g, lam)
     dev = torch.device("cuda")
+    tt = lambda x: torch.tensor(x, device=dev)       # noqa: E731
     st = torch.zeros(3, dtype=torch.float64, device=dev)
-    a, ret = gae(torch.tensor(r, device=dev), torch.tensor(v, device=dev), torch.tensor(es, device=dev),
-                 torch.tensor(lv, device=dev), torch.tensor(ld, device=dev), g, lam, stats=st)
+    a, ret = gae(tt(r), tt(v), tt(es), tt(lv), tt(ld), g, lam, stats=st)
     assert np.array_equal(a.cpu().numpy(), want_a)
     assert np.array_equal(ret.cpu().numpy(), want_r)
     s = st.cpu().numpy()
+    w = want_a.astype(np.float64)
     assert s[2] == T * N
-    assert abs(s[0] - want_a.astype(np.float64).sum()) < 1e-6 * abs(want_a).sum()
+    assert abs(s[0] - w.sum()) <= 1e-9 * np.abs(w).sum() + 1e-9
+    assert abs(s[1] - (w * w).sum()) <= 1e-9 * (w * w).sum()
+    st2 = torch.zeros(3, dtype=torch.float64, device=dev)
+    a2, ret2 = gae_dones(tt(r), tt(v), tt(dones.astype(np.uint8)), tt(lv), g, lam, stats=st2)
+    assert np.array_equal(a2.cpu().numpy(), want_a)
+    assert np.array_equal(ret2.cpu().numpy(), want_r)
+    assert np.allclose(st2.cpu().numpy(), s, rtol=1e-12, atol=1e-9)
 
 
-def test_baseline_size_properties():
-    """65,536 envs (BASELINE config 2): invariants that hold at any size --
-    determinism across two engines, a 64-env sample equal to the oracle,
-    well-formed observations, monotone step counters."""
+FULL_SIZE = [("multi", 5, 8, 65536, 64),       # BASELINE config 2 (1 GPU)
+             ("multi", None, 8, 32768, 64),    # config 4, one GPU's shard of 262,144
+             ("multi", 1, 16, 131072, 24)]     # config 5, one GPU's shard of 1,048,576
+
+
+@pytest.mark.parametrize("problem,mission,size,n,T", FULL_SIZE, ids=["cfg2_65536", "cfg4_32768", "cfg5_131072"])
+def test_full_size_matches_oracle(problem, mission, size, n, T):
+    """Every env at the BASELINE per-GPU sizes against the C oracle: per step the done flags,
+    the f64 rewards and the newest raw frame of all n envs; after T steps every env's full
+    state (grid, agent, carrying, step count, mission flags, stored reward, MT cursor, PCG64
+    state, target)."""
     _need_gpu()
     import oracle as O
     from mgx import MgxEngine
-    n, T = 65536, 64
-    e1 = MgxEngine(problem="multi", mission=5, size=8, n_envs=n)
-    e2 = MgxEngine(problem="multi", mission=5, size=8, n_envs=n)
-    e1.reset()
-    e2.reset()
-    g = torch.Generator(device="cuda")
-    g.manual_seed(3)
-    acts_log = []
+    ov = O.OracleVec(problem, mission, size, 4, n, 42)
+    eng = MgxEngine(problem=problem, mission=mission, size=size, n_envs=n, n_stack=4, terminal_mode="all",
+                    reward64=True)
+    r = ov.reset()
+    obs = eng.reset()
+    img, _, mi = EngineSource.newest(obs)
+    assert np.array_equal(img, r["image"]) and np.array_equal(mi, r["mission"])
+    acts = np.random.default_rng(2024).integers(0, 7, (T, n)).astype(np.int32)
+    acts_dev = torch.as_tensor(acts, device=eng.device)
     for t in range(T):
-        a = torch.randint(0, 7, (n,), device="cuda", generator=g)
-        acts_log.append(a.cpu().numpy())
-        o1 = e1.step(a)
-        o2 = e2.step(a)
-    for k in o1:
-        assert torch.equal(o1[k], o2[k]), k
-    img = o1["image"].view(n, 4, 3, 7, 7)[:, -1]
-    assert int(img[:, 0].max()) <= 10 and int(img[:, 1].max()) <= 5 and int(img[:, 2].max()) <= 2
-    assert torch.all(o1["direction"].view(n, 4, 4)[:, -1].sum(1) == 1)
-    # sample: envs [1000, 1064) equal the oracle (global index offset 1000)
-    ov = O.OracleVec("multi", 5, 8, 4, 64, 42, index_offset=1000)
-    ov.reset()
-    for t in range(T):
-        ov.step(acts_log[t][1000:1064])
-    a_, b_ = e1.dump_state(), ov.dump()
-    for k in ("grid", "agent", "step_count", "mtwords", "pcg"):
-        assert np.array_equal(a_[k][1000:1064], b_[k]), k
-    st = e1.stats()
-    assert st["steps"] == n * T and st["resets"] > n
-    e1.poll_error()
+        o = ov.step(acts[t])
+        obs = eng.step(acts_dev[t])
+        done = eng.done.cpu().numpy().astype(bool)
+        assert np.array_equal(done, (o["terminated"] | o["truncated"]).astype(bool)), t
+        assert np.array_equal(eng.reward64.cpu().numpy(), o["reward"]), t
+        img = obs["image"][:, -3:].permute(0, 2, 3, 1).cpu().numpy()
+        timg = eng.terminal_obs["image"][:, -3:].permute(0, 2, 3, 1).cpu().numpy()
+        assert np.array_equal(np.where(done[:, None, None, None], timg, img), o["image"]), t
+        assert np.array_equal(img[done], o["r_image"][done]), t
+    a, b = eng.dump_state(), ov.dump()
+    for k in ("grid", "agent", "carrying", "step_count", "mission_done", "mtwords", "pcg", "target"):
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a["stored_reward"], b["stored_reward"], equal_nan=True)
+    eng.poll_error()
 
 
-def test_sharded_engines_equal_one_engine():
-    """Env sharding: two handles owning global envs [0, n) and
-    [n, 2n) (env_index_offset) step exactly like one handle owning [0, 2n)."""
+def test_refill_accounting():
+    """mgx_stats: pre-generated episodes queued in the rings.  mgx_reset fills every ring to 2K;
+    each epoch the refill tops the rings up so that >= K stay queued at its join,
+    never more than D; episodes produced in an epoch = resets consumed + change of the queue."""
     _need_gpu()
     from mgx import MgxEngine
-    n, T = 4096, 96
-    whole = MgxEngine(problem="multi", mission=None, size=8, n_envs=2 * n)
-    parts = [MgxEngine(problem="multi", mission=None, size=8, n_envs=n, env_index_offset=r * n) for r in range(2)]
-    whole.reset()
-    for p in parts:
-        p.reset()
+    n = 4096
+    eng = MgxEngine(problem="multi", mission=None, size=8, n_envs=n, terminal_mode="none")
+    eng.reset()
+    K, D = eng.refill_every, eng.ring_depth
+    st = eng.stats()
+    assert st["queued"] == 2 * K * n and st["refill_launches"] == 1 and st["calls"] == 0
     g = torch.Generator(device="cuda")
-    g.manual_seed(11)
-    for t in range(T):
-        a = torch.randint(0, 7, (2 * n,), device="cuda", generator=g)
-        ow = whole.step(a)
-        op = [p.step(a[r * n:(r + 1) * n].contiguous()) for r, p in enumerate(parts)]
-        for k in ow:
-            assert torch.equal(ow[k], torch.cat([o[k] for o in op])), (t, k)
-        assert torch.equal(whole.reward, torch.cat([p.reward for p in parts])), t
-    sw = whole.stats()
-    sp = [p.stats() for p in parts]
-    assert sw["resets"] == sum(s["resets"] for s in sp)
-    whole.poll_error()
+    g.manual_seed(5)
+    for epoch in range(3):
+        prev = st
+        for _ in range(K):
+            eng.step(torch.randint(0, 7, (n,), device="cuda", generator=g, dtype=torch.int32))
+        st = eng.stats()
+        assert n * K <= st["queued"] <= n * D, (epoch, st)
+        produced = (st["resets"] - prev["resets"]) + (st["queued"] - prev["queued"])
+        assert produced >= st["resets"] - prev["resets"] > 0, (epoch, st, prev)
+        assert st["refill_launches"] == 2 + epoch and st["calls"] == K * (epoch + 1)
+    eng.poll_error()
 
 
 @pytest.mark.parametrize("n,terminal_mode", [(77, "all"), (130, "truncated")])

@@ -12,7 +12,7 @@ FIXTURES = TC.fixtures()
 
 
 def test_fixtures_present():
-    assert len(FIXTURES) == 32
+    assert len(FIXTURES) == 37
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=lambda p: p.split("/")[-1][:-4])

@@ -69,6 +69,40 @@ def test_mission_cache_same_features_and_grads():
         assert torch.allclose(a.grad, b.grad, atol=1e-5, rtol=1e-4), n1
 
 
+@pytest.mark.gpu
+def test_mission_cache_same_features_and_grads_gpu_large_batch():
+    """The same equality on the GPU at 40,000 rows: the uncached path splits the GRU batch into
+    16,384-row chunks (MIOpen RNN batch limit, CustomExtractor.gru_chunk) and the cached path
+    runs the distinct rows only (padded to a power of two); fp32 tolerance 1e-5 on features,
+    rtol 1e-3 on summed gradients (summation order differs)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.manual_seed(1)
+    p = ActorCriticPolicy().cuda()
+    q = ActorCriticPolicy(mission_cache=True).cuda()
+    q.load_state_dict(p.state_dict())
+    n = 40000
+    obs = {k: v.cuda() for k, v in _rand_obs(n, seed=4).items()}
+    # realistic stacks: a few hundred distinct missions, zero-filled older frames
+    lib = torch.randint(0, 32, (300, 32), dtype=torch.uint8, device="cuda")
+    pick = torch.randint(0, 300, (n, 4), device="cuda")
+    m = lib[pick].reshape(n, 128)
+    m[: n // 3, :64] = 0
+    obs["mission"] = m
+    assert p.features_extractor.gru_chunk < n
+    pre = preprocess(obs)
+    f1 = p.features_extractor(pre)
+    f2 = q.features_extractor(pre)
+    assert torch.allclose(f1, f2, atol=1e-5, rtol=1e-5)
+    acts = torch.randint(0, 7, (n,), device="cuda")
+    v1, l1, _ = p.evaluate_actions(obs, acts)
+    v2, l2, _ = q.evaluate_actions(obs, acts)
+    (v1.sum() + l1.sum()).backward()
+    (v2.sum() + l2.sum()).backward()
+    for (n1, a), (_, b) in zip(p.named_parameters(), q.named_parameters()):
+        assert torch.allclose(a.grad, b.grad, atol=1e-3, rtol=1e-3), n1
+
+
 def _fill_buffer(T, N, seed):
     g = torch.Generator().manual_seed(seed)
     buf = RolloutBuffer(T, N, 4, "cpu")

@@ -22,11 +22,13 @@ def fixtures():
 
 def fixture_cfg(d):
     S, n, T, seed, mission, nobj = [int(x) for x in d["meta"]]
-    stw, obst = [int(x) for x in d["env_flags"]] if "env_flags" in d else (1, 0)
+    flags = [int(x) for x in d["env_flags"]] if "env_flags" in d else [1, 0]
+    stw, obst = flags[0], flags[1]
+    ado = flags[2] if len(flags) > 2 else 0          # all_doors_open (third flag, added in round 2)
     pct = float(d["percent_obstacles"]) if "percent_obstacles" in d else 0.05
     return dict(problem=str(d["problem"]), mission=None if mission < 0 else mission, size=S,
                 num_objects=nobj, n_envs=n, seed=seed, see_through_walls=bool(stw), obstacles=bool(obst),
-                percent_obstacles=pct), T
+                percent_obstacles=pct, all_doors_open=bool(ado)), T
 
 
 def _eq(a, b):
@@ -95,7 +97,8 @@ class OracleSource:
         self.v = O.OracleVec(cfg["problem"], cfg["mission"], cfg["size"], cfg["num_objects"], cfg["n_envs"],
                              cfg["seed"], see_through_walls=cfg.get("see_through_walls", True),
                              obstacles=cfg.get("obstacles", False),
-                             percent_obstacles=cfg.get("percent_obstacles", 0.05))
+                             percent_obstacles=cfg.get("percent_obstacles", 0.05),
+                             all_doors_open=cfg.get("all_doors_open", False))
 
     def reset(self):
         return self.v.reset()
