@@ -239,7 +239,8 @@ def main_ppo(args, world, rank, local, dev):
         print(json.dumps({
             "metric": "PPO env-steps/sec (rollout + train), PKP 8x8, 65k envs/GPU",
             "value": K * n * cfg.horizon * world / wall, "unit": "env-steps/s", "n_gpus": world, "steps": K,
-            "warmup": W, "ms_per_step": wall * 1e3 / K, "higher_is_better": True, "scaling": "weak",
+            "warmup": W,
+            "warmup_requested": args.warmup, "ms_per_step": wall * 1e3 / K, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8 env / fp32 policy",
             "data": "synthetic (policy-sampled actions; env i seeded 42+i; random-init policy)",
             "config": {"workload": "PKP 8x8 full PPO loop, %d envs/GPU (BASELINE config 3)" % n,
@@ -340,7 +341,9 @@ def main():
                     refill_every=E or 0, refill_cap=args.refill_cap, ring_depth=args.ring_depth)
     E = eng.refill_every
     H = pick_horizon(K, E if aligned else None, args.horizon or 0)
-    W = -(-args.warmup // E) * E                         # warm-up rounded up to whole refill epochs
+    # warm-up: whole refill epochs, and at least 128 steps -- the rings start at 2E episodes and
+    # fill towards D, so a shorter warm-up would time the fill-up, not the steady state
+    W = -(-max(args.warmup, 128) // E) * E
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     P = args.probe
@@ -372,6 +375,7 @@ def main():
 
     nchunks = K // H
     graphs = []
+    forks0 = eng.stats()["refill_launches"]
     if args.graph:
         # one hipGraph per horizon chunk (launch-bound loop -> one replay each); a chunk is whole
         # refill epochs, so each graph holds its forks and joins (self-contained capture)
@@ -385,6 +389,9 @@ def main():
                 graphs.append(gr)
         torch.cuda.synchronize(dev)
     st0 = eng.stats()
+    # refill launches inside the timed region: the forks the steps enqueued (captured once in the
+    # graphs, replayed once each; eagerly, counted as they run)
+    forks = (st0["refill_launches"] - forks0) if graphs else None
     hist = torch.zeros((nchunks, 3), dtype=torch.float64, device=dev)
     if world > 1:
         dist.barrier()
@@ -469,6 +476,7 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": W,
+            "warmup_requested": args.warmup,
             "ms_per_step": wall_max * 1e3 / K,
             "higher_is_better": True,
             "scaling": "weak",
@@ -483,7 +491,7 @@ def main():
                        "timed": "%d steps = %d whole refill epochs%s; GAE + adv-stat %s every %d steps" % (
                            K, K // E, "" if aligned else " + a joined partial one",
                            "all-reduce (%s)" % dist.get_backend() if world > 1 else "accumulation", H)},
-            "window": {"refill_launches": st1["refill_launches"] - st0["refill_launches"],
+            "window": {"refill_launches": forks if forks is not None else st1["refill_launches"] - st0["refill_launches"],
                        "episodes_produced": (st1["resets"] - st0["resets"]) + (st1["queued"] - st0["queued"]),
                        "episodes_consumed": st1["resets"] - st0["resets"],
                        "gae_launches": nchunks},

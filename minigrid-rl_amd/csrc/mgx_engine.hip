@@ -1148,7 +1148,7 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
 // 3*GAE_U loads in flight.  DONES: the compact form -- `es` is u8 dones[T][N] (done after
 // step t), next_non_terminal(t) = 1 - dones[t]; otherwise SB3's f32 episode_starts[T][N]
 // plus last_dones (next_non_terminal(t) = 1 - episode_starts[t+1], 1 - last_dones at T-1).
-constexpr int GAE_U = 8;
+constexpr int GAE_U = 32;     // steps per chunk: 3*32 loads in flight per lane (one wave per SIMD at N=65,536)
 
 template <bool DONES>
 struct GaeChunk {
@@ -1165,9 +1165,10 @@ __device__ __forceinline__ void gae_load(GaeChunk<DONES> &c, const float *__rest
         const int64_t tt = t - j;
         if (tt >= 0) {
             const int64_t k = tt * N + i;
-            c.r[j] = r[k];
-            c.v[j] = v[k];
-            c.e[j] = DONES ? (float)static_cast<const uint8_t *>(es)[k] : static_cast<const float *>(es)[k];
+            c.r[j] = __builtin_nontemporal_load(r + k);
+            c.v[j] = __builtin_nontemporal_load(v + k);
+            c.e[j] = DONES ? (float)__builtin_nontemporal_load(static_cast<const uint8_t *>(es) + k)
+                           : __builtin_nontemporal_load(static_cast<const float *>(es) + k);
         }
     }
 }
@@ -1197,8 +1198,8 @@ __global__ __launch_bounds__(256) void mgx_gae_kernel(const float *__restrict__ 
                     const float vt = cur.v[j];
                     const float delta = (cur.r[j] + (g * nv) * nnt) - vt;
                     last = delta + (c * nnt) * last;
-                    adv[k] = last;
-                    ret[k] = last + vt;
+                    __builtin_nontemporal_store(last, adv + k);
+                    __builtin_nontemporal_store(last + vt, ret + k);
                     s1 += (double)last;
                     s2 += (double)last * (double)last;
                     if (!DONES) nnt = 1.0f - cur.e[j];   // for step t-1: 1 - episode_starts[t]

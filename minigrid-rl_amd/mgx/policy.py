@@ -80,7 +80,9 @@ class CustomExtractor(nn.Module):
         arch = DEFAULT_ARCH if arch is None else arch
         self.n_frames_stack = n_frames_stack
         self.mission_cache = mission_cache
-        self.gru_chunk = 16384          # MIOpen's RNN rejects very large batches (miopenStatusBadParm)
+        # MIOpen's RNN rejects batches of 16,384 rows and more (miopenStatusBadParm, "Lengths must be
+        # > 0"; 12,288 is accepted, with and without autograd: tools/gru_batch_probe.py on MI355X)
+        self.gru_chunk = 8192
         self.aten_gru = os.environ.get("MGX_ATEN_GRU", "0") == "1"
         self.gru = False
         ext = {}
@@ -119,6 +121,11 @@ class CustomExtractor(nn.Module):
             return h[-1]
         return seq(tok)
 
+    def _mission_chunked(self, seq, tok):
+        if tok.shape[0] <= self.gru_chunk:
+            return self._mission(seq, tok)
+        return torch.cat([self._mission(seq, c) for c in tok.split(self.gru_chunk)])
+
     def forward(self, obs):
         outs = []
         for key, seq in self.extractors.items():
@@ -134,10 +141,9 @@ class CustomExtractor(nn.Module):
                     ub = max(64, 1 << (u - 1).bit_length())
                     first = torch.zeros(ub, dtype=torch.int64, device=tok.device)
                     first.scatter_(0, inv, torch.arange(tok.shape[0], device=tok.device))
-                    out = self._mission(seq, tok.index_select(0, first)).index_select(0, inv)
+                    out = self._mission_chunked(seq, tok.index_select(0, first)).index_select(0, inv)
                 else:
-                    out = torch.cat([self._mission(seq, c) for c in tok.split(self.gru_chunk)]) \
-                        if tok.shape[0] > self.gru_chunk else self._mission(seq, tok)
+                    out = self._mission_chunked(seq, tok)
             else:
                 out = seq(x)
             if out.dim() > 2:

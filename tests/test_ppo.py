@@ -72,9 +72,9 @@ def test_mission_cache_same_features_and_grads():
 @pytest.mark.gpu
 def test_mission_cache_same_features_and_grads_gpu_large_batch():
     """The same equality on the GPU at 40,000 rows: the uncached path splits the GRU batch into
-    16,384-row chunks (MIOpen RNN batch limit, CustomExtractor.gru_chunk) and the cached path
-    runs the distinct rows only (padded to a power of two); fp32 tolerance 1e-5 on features,
-    rtol 1e-3 on summed gradients (summation order differs)."""
+    8,192-row chunks (MIOpen's RNN refuses 16,384 rows; CustomExtractor.gru_chunk) and the cached
+    path runs the distinct rows only (padded to a power of two, chunked the same way); fp32
+    tolerance 1e-5 on features, rtol 1e-3 on summed gradients (summation order differs)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     torch.manual_seed(1)
@@ -83,9 +83,9 @@ def test_mission_cache_same_features_and_grads_gpu_large_batch():
     q.load_state_dict(p.state_dict())
     n = 40000
     obs = {k: v.cuda() for k, v in _rand_obs(n, seed=4).items()}
-    # realistic stacks: a few hundred distinct missions, zero-filled older frames
-    lib = torch.randint(0, 32, (300, 32), dtype=torch.uint8, device="cuda")
-    pick = torch.randint(0, 300, (n, 4), device="cuda")
+    # stacks drawn from 4,000 mission rows (>8,192 distinct stacks), a third with zero-filled older frames
+    lib = torch.randint(0, 32, (4000, 32), dtype=torch.uint8, device="cuda")
+    pick = torch.randint(0, 4000, (n, 4), device="cuda")   # > 8,192 distinct stacks: cache path chunks too
     m = lib[pick].reshape(n, 128)
     m[: n // 3, :64] = 0
     obs["mission"] = m
