@@ -389,13 +389,26 @@ __device__ __forceinline__ void mt_sync(Gen<NW> &G) {
 // field f of a word that is f < n << (5 - k).  Ten fields at once: guard-bit SWAR
 // subtract, first set guard = first accepted word.  One pass almost always suffices
 // (a lane needs another only after ten rejections), so lanes do not diverge here.
+struct RbConst {            // randbelow(n) constants: field shift 5 - bit_length(n), SWAR compare word
+    uint64_t c1;
+    uint32_t sh;
+};
+__device__ __forceinline__ RbConst rb_const(uint32_t n) {
+    const uint32_t sh = 5u - (uint32_t)(32 - __clz(n));
+    return RbConst{(uint64_t)(32u + (n << sh) - 1u) * MT_REP, sh};   // per slot: 32 + c - 1
+}
+template <int NW>
+__device__ __forceinline__ int randbelow_c(Gen<NW> &G, const RbConst K);
 template <int NW>
 __device__ __forceinline__ int randbelow(Gen<NW> &G, uint32_t n) {
     GCOUNT(G, 24);
     if (n >= 32u) { G.err |= 8u; return 0; }        // excluded by validation (n < 32 always)
-    const int k = 32 - __clz(n);
-    const uint32_t sh = 5 - k;
-    const uint64_t c1 = (uint64_t)(32u + (n << sh) - 1u) * MT_REP;  // per slot: 32 + c - 1
+    return randbelow_c(G, rb_const(n));
+}
+template <int NW>
+__device__ __forceinline__ int randbelow_c(Gen<NW> &G, const RbConst K) {
+    const uint64_t c1 = K.c1;
+    const uint32_t sh = K.sh;
     for (;;) {
         GCOUNT(G, 21);
         const int o6 = 6 * G.go;
@@ -750,14 +763,16 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
         else { c3 -= ndec; n = c3; }
         npack |= (uint32_t)(n > 0 ? n : 0) << (8 * r);
     }
-    // The keys and objects of all rooms as ONE task sequence executed by one flat loop:
-    // every iteration makes one placement attempt for every lane, whatever room/task the
-    // lane is at, so lanes no longer wait for each other at room and object boundaries
-    // (the nested room/key/object loops were the generator's dominant divergence).
-    // Each lane still draws exactly the reference's sequence:
-    //   for room r: [key A] [key B] then n_r x { choice(obj_choice); position loop }.
-    int r = 0, phase = 0, kleft = 0, kx = -1, ky = -1, rej = 0, ot = 0, ocn = 0;
-    bool chosen = false, fin = false;
+    // The keys and objects of all rooms as ONE task sequence: every outer iteration places
+    // one key or object for every lane, whatever room/task the lane is at (lanes do not wait
+    // for each other at room boundaries).  Each lane still draws exactly the reference's
+    // sequence:  for room r: [key A] [key B] then n_r x { choice(obj_choice); position loop }.
+    // The rejection loop `while True: p = (randint(x0,x1), randint(y0,y1)); if ok(p): break`
+    // is the tight inner loop: the cells a placement must avoid are one precomputed bit set,
+    // so a rejected draw costs two SWAR randbelow and one bit test -- the lanes that need many
+    // draws (the wave waits for them) no longer re-run the task set-up per draw.
+    int r = 0, phase = 0, kleft = 0, kx = -1, ky = -1;
+    bool fin = false;
 #pragma unroll 1
     for (int it = 0; it < 12; it++) {            // advance to the first task (bounded)
         if (phase == 0) { if ((keymask >> (2 * r)) & 1) break; phase = 1; }
@@ -773,7 +788,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
         int x0, x1, y0, y1;
         room_rect(nr, r, mid, S, x0, x1, y0, y1);
         const bool is_key = phase < 2;
-        int cname, ox = -1, oy = -1;
+        int cname, ot = T_KEY, ox = -1, oy = -1;
         bool chk = false, kib = false;
         if (is_key) {
             int kA, kB;
@@ -782,55 +797,71 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
             cname = di & 7;
             kib = (di >> 4) & 1;
             if (phase == 1) { ox = kx; oy = ky; }
-            if (rej == 0 && !rect_has_free(G, x0, x1, y0, y1, false, gx, gy, chk ? G.ax : -1, chk ? G.ay : -1, ox, oy)) {
+            if (!rect_has_free(G, x0, x1, y0, y1, false, gx, gy, chk ? G.ax : -1, chk ? G.ay : -1, ox, oy)) {
                 live_lock(G); return;
             }
         } else {
-            if (!chosen) {
-                if (oc == 0) { G.err |= 8u; break; }
-                const int b = mask_choice(G, oc);
-                if (G.abort) return;
-                oc &= ~(1u << b);
-                ot = MULTI_TYPES[b / 6];
-                ocn = b % 6;
-                chosen = true;
-                if (!rect_has_free(G, x0, x1, y0, y1, true, G.ax, G.ay, -1, -1, -1, -1)) { live_lock(G); return; }
-            }
-            cname = ocn;
+            if (oc == 0) { G.err |= 8u; break; }
+            const int b = mask_choice(G, oc);
+            if (G.abort) return;
+            oc &= ~(1u << b);
+            ot = MULTI_TYPES[b / 6];
+            cname = b % 6;
+            if (!rect_has_free(G, x0, x1, y0, y1, true, G.ax, G.ay, -1, -1, -1, -1)) { live_lock(G); return; }
         }
-        const int x = randint(G, x0, x1);
-        const int y = randint(G, y0, y1);
-        if (G.abort) return;
-        const bool bad = is_key ? ((x == gx && y == gy) || (chk && x == G.ax && y == G.ay) || (x == ox && y == oy) ||
-                                   next2door(G, x, y))
-                                : (occupied(G, y * S + x) || (x == G.ax && y == G.ay) || next2door(G, x, y));
-        if (bad) {
-            if (++rej == SAT_PROBE) {            // provably unsatisfiable loop -> live-lock policy
-                bool sat = false;
-                for (int xx = x0; xx <= x1 && !sat; xx++)
-                    for (int yy = y0; yy <= y1 && !sat; yy++)
-                        sat = is_key ? !((xx == gx && yy == gy) || (chk && xx == G.ax && yy == G.ay) ||
-                                         (xx == ox && yy == oy) || next2door(G, xx, yy))
-                                     : !(occupied(G, yy * S + xx) || (xx == G.ax && yy == G.ay) || next2door(G, xx, yy));
-                if (!sat) { live_lock(G); return; }
+        // cells this placement rejects: key -> goal, [agent], [the other key], next to a door;
+        // object -> occupied, agent, next to a door
+        const int ex0 = is_key ? gx : G.ax, ey0 = is_key ? gy : G.ay;
+        const int ex1 = (is_key && !chk) ? -1 : G.ax, ey1 = (is_key && !chk) ? -1 : G.ay;
+        const RbConst kx_ = rb_const((uint32_t)(x1 - x0 + 1)), ky_ = rb_const((uint32_t)(y1 - y0 + 1));
+        int x, y;
+        if constexpr (NW <= 2) {
+            Bits<NW> bad = G.dn;
+            if (!is_key) { bad.w0 |= G.occ.w0; if (NW > 1) bad.w1 |= G.occ.w1; }
+            bad.set(ey0 * S + ex0);
+            if (ex1 >= 0) bad.set(ey1 * S + ex1);
+            if (ox >= 0) bad.set(oy * S + ox);
+#pragma unroll 1
+            for (;;) {                            // satisfiable (checked above): ends, or hits the word cap
+                GCOUNT(G, 21);
+                x = x0 + randbelow_c(G, kx_);
+                y = y0 + randbelow_c(G, ky_);
+                if (G.abort) return;
+                if (!bad.test(y * S + x)) break;
             }
-            continue;
+        } else {
+            int rej = 0;
+#pragma unroll 1
+            for (;;) {
+                GCOUNT(G, 21);
+                x = x0 + randbelow_c(G, kx_);
+                y = y0 + randbelow_c(G, ky_);
+                if (G.abort) return;
+                const bool bad = (x == ex0 && y == ey0) || (x == ex1 && y == ey1) || (x == ox && y == oy) ||
+                                 (!is_key && occupied(G, y * S + x)) || next2door(G, x, y);
+                if (!bad) break;
+                if (++rej == SAT_PROBE) {            // provably unsatisfiable loop -> live-lock policy
+                    bool sat = false;
+                    for (int xx = x0; xx <= x1 && !sat; xx++)
+                        for (int yy = y0; yy <= y1 && !sat; yy++)
+                            sat = !((xx == ex0 && yy == ey0) || (xx == ex1 && yy == ey1) || (xx == ox && yy == oy) ||
+                                    (!is_key && occupied(G, yy * S + xx)) || next2door(G, xx, yy));
+                    if (!sat) { live_lock(G); return; }
+                }
+            }
         }
         // commit the placement, then advance to the next task
         const int cidx = cn2idx(cname);
+        const int t = is_key ? (kib ? T_BOX : T_KEY) : ot;
+        put(G, x, y, mk_code(t, cidx, (is_key && kib) ? 1 : 0));
+        add_obj(G, t, cname, x, y);
         if (is_key) {
-            if (kib) { put(G, x, y, mk_code(T_BOX, cidx, 1)); add_obj(G, T_BOX, cname, x, y); }
-            else { put(G, x, y, mk_code(T_KEY, cidx, 0)); add_obj(G, T_KEY, cname, x, y); }
             if (phase == 0) { kx = x; ky = y; }
             phase++;
             if (phase == 2) kleft = (npack >> (8 * r)) & 0xFF;
         } else {
-            put(G, x, y, mk_code(ot, cidx, 0));
-            add_obj(G, ot, cname, x, y);
-            chosen = false;
             kleft--;
         }
-        rej = 0;
 #pragma unroll 1
         for (int k2 = 0; k2 < 12; k2++) {
             if (phase == 1) { if ((keymask >> (2 * r + 1)) & 1) break; phase = 2; kleft = (npack >> (8 * r)) & 0xFF; }

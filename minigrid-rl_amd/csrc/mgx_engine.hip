@@ -1063,7 +1063,7 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
 // order the env will consume them, so RNG streams advance as in the reference.
 // One wave per workgroup; all LDS is lane-private (grid row + MT window + objs).
 template <int NW, bool EXT>
-__global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
+__device__ __forceinline__ void refill_body(const KParams &p) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int tid = threadIdx.x;
     const int64_t e = (int64_t)blockIdx.x * 64 + tid;
@@ -1136,6 +1136,15 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) {
         }
         if (err) atomicOr(p.err, err);
     }
+}
+
+template <int NW, bool EXT>
+__global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) { refill_body<NW, EXT>(p); }
+// The default variant (S <= 8, no EXT features) runs beside three step workgroups per CU:
+// 176 + 3 x 112 VGPRs per SIMD lane fill the 512-entry file exactly.
+template <>
+__global__ __launch_bounds__(64, 3) void mgx_refill_kernel<1, false>(KParams p) {
+    refill_body<1, false>(p);
 }
 
 // ================================================================ GAE kernel
