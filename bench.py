@@ -76,6 +76,8 @@ def parse():
                          "largest whole-epoch divisor of --steps up to 1024; ppo: default 16)")
     ap.add_argument("--batch-size", type=int, default=65536, help="ppo: minibatch size")
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
+    ap.add_argument("--layout", default="compact", choices=["compact", "sb3"],
+                    help="ppo: rollout storage (compact rows + gather, or materialised SB3 stacks)")
     args = ap.parse_args()
     presets = {2: dict(mission="5", size=8, n_envs=65536), 4: dict(mission="None", size=8, n_envs=32768),
                5: dict(mission="1", size=16, n_envs=131072)}
@@ -179,14 +181,15 @@ def _allreduce(t, op):
 def main_ppo(args, world, rank, local, dev):
     """BASELINE config 3: PPO(CustomPPOPolicy) on PKP 8x8 with the engine (mgx/ppo.py)."""
     from mgx.policy import ActorCriticPolicy
-    from mgx.ppo import PPOConfig, RolloutCollector, Trainer
+    from mgx.ppo import PPOConfig, Trainer, make_collector
     from mgx import MgxEngine
     mission = None if args.mission == "None" else int(args.mission)
     if args.mission == "5" and args.problem == "multi":
         mission = 2                                   # config 3 is PKP ('pick up')
     n = args.n_envs
     cfg = PPOConfig(n_envs=n, horizon=args.horizon, batch_size=args.batch_size, n_epochs=args.epochs,
-                    env=dict(problem=args.problem, mission=mission, size=args.size, num_objects=4))
+                    env=dict(problem=args.problem, mission=mission, size=args.size, num_objects=4),
+                    layout=args.layout)
     torch.manual_seed(cfg.seed + rank)
     eng = MgxEngine(n_envs=n, seed=cfg.seed, env_index_offset=rank * n, n_stack=cfg.n_frames_stack,
                     terminal_mode="truncated", mission_dtype=torch.uint8, device=dev, **cfg.env)
@@ -196,8 +199,17 @@ def main_ppo(args, world, rank, local, dev):
     if group is not None:
         for p_ in pol.parameters():
             dist.broadcast(p_.data, 0)
-    col = RolloutCollector(eng, pol, cfg)
+    col = make_collector(eng, pol, cfg)
     tr = Trainer(pol, cfg, group)
+    if rank == 0:                       # heartbeat: the first iteration compiles MIOpen kernels for minutes
+        import threading
+        t_start = time.perf_counter()
+
+        def beat():
+            while True:
+                time.sleep(30)
+                print("ppo: running, %.0fs" % (time.perf_counter() - t_start), file=sys.stderr, flush=True)
+        threading.Thread(target=beat, daemon=True).start()
     col.start()
     K, W = args.steps, args.warmup
     total = (K + W) * n * cfg.horizon * world
@@ -247,7 +259,8 @@ def main_ppo(args, world, rank, local, dev):
                        "problem": args.problem, "mission": mission, "size": args.size, "envs_per_gpu": n,
                        "horizon": cfg.horizon, "batch_size": cfg.batch_size, "n_epochs": cfg.n_epochs,
                        "minibatches_per_epoch": n * world * cfg.horizon // cfg.batch_size // world,
-                       "mission_cache": cfg.mission_cache, "parallelism": "env-sharded dp%d" % world},
+                       "mission_cache": cfg.mission_cache, "layout": cfg.layout,
+                       "parallelism": "env-sharded dp%d" % world},
             "phases_s_per_iter": {"collect": tc / K, "train": tt / K},
             "roofline": None,
         }), flush=True)

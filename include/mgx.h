@@ -149,6 +149,51 @@ mgx_status mgx_set_seed(mgx_handle *h, int64_t seed);
 mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes,
                     const mgx_step_out *out, void *stream);
 
+/* ---- Compact rollout layout ------------------------------
+ * One observation = one 148-B ROW (byte 0: agent direction 0..3; bytes 1..147: the
+ * [c][vx][vy] frame, VecTransposeImage order) + one mission-id byte (mgx_mission_text;
+ * tokens = TokenizeVocabWrapper of that text).  A rollout buffer is [T][N] rows; the
+ * SB3 stacked observation of any (t, env) is rebuilt by mgx_gather from rows t-n_stack+1..t
+ * and the episode-start flags (VecFrameStack zero-fills before an episode's first obs).
+ * 150 B per env-step instead of 588 + 16 + 32*n_stack*(1|8) B; no stack roll per step. */
+typedef struct mgx_compact_out {
+    uint8_t *row_dev;             /* u8 [N][148]: the observation after this step (the new
+                                     episode's first one where done) */
+    uint8_t *mission_id_dev;      /* u8 [N]: its mission id */
+    uint8_t *terminal_row_dev;    /* u8 [N][148]: the final observation of each episode that ended
+                                     (written where terminal_mode selects; its mission id is the
+                                     previous row's) */
+    float *reward_dev;            /* as mgx_step_out */
+    double *reward64_dev;
+    uint8_t *terminated_dev;
+    uint8_t *truncated_dev;
+    uint8_t *done_dev;            /* u8 [N]: done of this step = start flag of the row written */
+    float *ep_return_dev;
+    int32_t *ep_len_dev;
+    int32_t *livelock_dev;
+} mgx_compact_out;
+
+/* mgx_step with compact outputs (same transition, RNG, auto-reset and refill epochs as
+ * mgx_step; the two may not be mixed on one handle between resets).  Needs the ring. */
+mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_bytes, const mgx_compact_out *out,
+                            void *stream);
+
+/* The current observation of every env as compact rows (e.g. row 0 after mgx_reset). */
+mgx_status mgx_observe_compact(mgx_handle *h, uint8_t *row_dev, uint8_t *mission_id_dev, void *stream);
+
+/* Stacked observations (VecFrameStack(n_stack) of the handle) of n_samples (t, env) pairs from
+ * a compact buffer: rows_dev u8 [R][n_envs][148], mission_ids_dev / starts_dev u8 [R][n_envs]
+ * (start = the row is an episode's first observation); index_dev i64 [n_samples] = t*n_envs +
+ * env of the newest row, which must have n_stack-1 rows before it.  terminal_rows_dev (u8
+ * [n_envs][148], optional): the newest frame is env's terminal row and the older ones start at
+ * row index (SB3's stacked terminal_observation).  Outputs (device): image [n][3*n_stack][7][7]
+ * u8 or f32 (= u8 / 255, SB3 preprocess_obs), direction [n][4*n_stack] u8 or f32 one-hot,
+ * mission [n][32*n_stack] u8 tokens. */
+mgx_status mgx_gather(const mgx_handle *h, const uint8_t *rows_dev, const uint8_t *mission_ids_dev,
+                      const uint8_t *starts_dev, int64_t n_envs, const int64_t *index_dev, int64_t n_samples,
+                      const uint8_t *terminal_rows_dev, void *image_dev, int image_f32, void *direction_dev,
+                      int direction_f32, uint8_t *mission_dev, void *stream);
+
 /* Makes `stream` wait for the in-flight refill, if any (no host sync). */
 mgx_status mgx_join(mgx_handle *h, void *stream);
 

@@ -426,12 +426,16 @@ __device__ __forceinline__ void render13(const uint8_t *grids, int S, int le, in
 // (mgx_refill_kernel); an empty ring defers the env to mgx_fixup_kernel, which
 // runs right after on the same stream.  Keeping the generator out of this
 // kernel keeps it register-light (high occupancy hides its memory latency).
-template <typename ActT>
+// COMPACT: the compact rollout layout (mgx_step_compact) instead of the SB3 stacks -- each
+// env's new observation is ONE 148-B row (byte 0 direction, bytes 1..147 the [c][vx][vy]
+// frame: the fast path's LDS frame row, copied out verbatim) plus its mission id byte; no
+// stack is read or rolled (mgx_gather rebuilds stacks from consecutive rows on demand).
+template <typename ActT, bool COMPACT>
 __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, KOut o, const ActT *__restrict__ actions) {
     extern __shared__ __align__(16) uint8_t smem[];
-    // fast path (n_stack == 4): smem = frame rows [64][148] (new frame at bytes 1..147);
-    // staged path: smem = image stacks [64][IMG] (new frame in slot 0 of a row).
-    const bool fast = p.fast_roll;
+    // fast path (n_stack == 4) and COMPACT: smem = frame rows [64][148] (new frame at bytes
+    // 1..147); staged path: smem = image stacks [64][IMG] (new frame in slot 0 of a row).
+    const bool fast = !COMPACT && p.fast_roll;
     uint8_t *s_stk = smem;
     uint8_t *s_grid = smem + p.stk_step;         // grids, chunk-major [GS/16][64 lanes][16 B] (cm_off)
     uint8_t *s_pgrid = s_grid + BLOCK_ENVS * p.GS;   // popped episodes' grids, same layout
@@ -444,7 +448,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     uint4 *s_ptokB = s_ptokA + BLOCK_ENVS;
     uint4 *s_prng = s_ptokB + BLOCK_ENVS;        // [2][64] the popped episode's RNG snapshot
     const int IMG = p.img_bytes;
-    const int FSTRIDE = fast ? FROW : IMG, FOFF = fast ? 1 : 0;
+    const int FSTRIDE = (fast || COMPACT) ? FROW : IMG, FOFF = (fast || COMPACT) ? 1 : 0;
     __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params ax | ay<<8 | dir<<16 | carry<<24
     __shared__ uint8_t s_done[BLOCK_ENVS];
     __shared__ uint8_t s_term[BLOCK_ENVS];       // done env whose stacked terminal_observation is written
@@ -515,7 +519,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         if (kt + 37 < limit) tq37 = g32in[kt + 37];
     }
     // (b) staged path: the whole old stacks -> LDS
-    if (!fast) {
+    if (!fast && !COMPACT) {
         const uint8_t *gimg = o.img + e0 * (int64_t)IMG;
         const int nbytes = ne * IMG;
         const int n16 = nbytes >> 4;
@@ -533,8 +537,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         const uint4 sv = reinterpret_cast<const uint4 *>(p.state)[e0 + le0];
         __builtin_memcpy(&st, &sv, sizeof st);
         a = (int)actions[e0 + le0];
-        odir = p.n_stack == 4 ? reinterpret_cast<const uint4 *>(o.dir)[e0 + le0]
-                              : reinterpret_cast<const uint4 *>(p.state)[0];      // unused
+        odir = (!COMPACT && p.n_stack == 4) ? reinterpret_cast<const uint4 *>(o.dir)[e0 + le0]
+                                            : reinterpret_cast<const uint4 *>(p.state)[0];      // unused
         rhead = p.ring_head[e0 + le0];           // allocated (zeros) even without a ring
         rpub = p.ring_pub[e0 + le0];
         mrange = p.range_cur[p.has_move ? e0 + le0 : 0];
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // if the step does end it.  Envs whose stack is still filling fetch their mission's tokens.
     bool spec = false;
     if (tid < ne) {
-        if (st.frames < p.n_stack) {
+        if (!COMPACT && st.frames < p.n_stack) {
             const uint4 *t = reinterpret_cast<const uint4 *>(p.mtok + st.mission_id * 32);
             __builtin_amdgcn_global_load_lds(t, s_tokA, 16, 0, 0);
             __builtin_amdgcn_global_load_lds(t + 1, s_tokB, 16, 0, 0);
@@ -607,7 +611,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         // so the next episode is already in LDS (phase 1c)
         const bool done_e = (a == A_FORWARD && (ft == T_GOAL || ft == T_LAVA)) || a == A_DONE || sc >= ms;
         const bool avail = done_e && spec;
-        const bool filling = !done_e && st.frames < p.n_stack;
+        const bool filling = !COMPACT && !done_e && st.frames < p.n_stack;
         double rew = 0.0;
         switch (a) {                                   // MiniGridEnv.step (3P)
             case A_LEFT: dir = (dir + 3) & 3; break;
@@ -676,7 +680,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         done = term || trunc;
         const bool tw = done && (p.terminal_mode == MGX_TERMINAL_ALL ||
                                  (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term));
-        if (tw) {                                      // stacked terminal_observation: dir + mission
+        if (tw && !COMPACT) {                          // stacked terminal_observation: dir + mission
             // (rare; before the pop rewrites this env's direction row)
             const int frames = min((int)st.frames + 1, p.n_stack);
             if (p.n_stack == 4)
@@ -704,7 +708,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             ns.mission_done = (uint8_t)mdone; ns.frames = 1; ns.flags = 0; ns.pad = 0;
             p.state[e] = ns;
             s_rp2[tid] = (uint32_t)nax | ((uint32_t)nay << 8) | ((uint32_t)ndir << 16);
-            dir_stack_fresh(o.dir, e, p.n_stack, ndir);
+            if (COMPACT) static_cast<uint8_t *>(o.mis)[e] = mid;
+            else dir_stack_fresh(o.dir, e, p.n_stack, ndir);
             if (o.livelock) o.livelock[e] = (int)h.z;
             dirty = true;
             popped = true;
@@ -727,7 +732,9 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         if (o.ep_len) o.ep_len[e] = sc;
         if (!done) {
             const int frames = min((int)st.frames + 1, p.n_stack);
-            if (p.n_stack == 4)
+            if (COMPACT)
+                static_cast<uint8_t *>(o.mis)[e] = st.mission_id;
+            else if (p.n_stack == 4)
                 reinterpret_cast<uint4 *>(o.dir)[e] = make_uint4(odir.y, odir.z, odir.w, 1u << (8 * dir));
             else
                 dir_stack_roll(o.dir, o.dir, e, p.n_stack, dir);
@@ -764,7 +771,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // ---- phase 2b: mission stacks first (their stores drain during the render), block-
     // cooperative and coalesced: fresh stacks of popped envs (zeros + tokens in the newest
     // slot), then the one flipping slot of filling envs
-    {
+    if (!COMPACT) {
         const int K = p.n_stack, CPS = p.mission64 ? 16 : 2, per = K * CPS;
         const uint8_t *tA = reinterpret_cast<const uint8_t *>(s_ptokA), *tB = reinterpret_cast<const uint8_t *>(s_ptokB);
         const int tot_d = s_npop * per;
@@ -800,7 +807,17 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             if (tid < ne && s_term[tid]) apply_vis(s_stk + tid * FSTRIDE + FOFF);
             __syncthreads();
         }
-        {
+        if (COMPACT) {                                // terminal row: byte 0 direction, then the frame
+            if (tid < ne && s_term[tid]) s_stk[tid * FROW] = (uint8_t)((s_rp[tid] >> 16) & 3);
+            __syncthreads();
+            const int le = tid >> 2, q = tid & 3;
+            if (le < ne && s_term[le]) {
+                const uint32_t *fr = reinterpret_cast<const uint32_t *>(s_stk + le * FROW);
+                uint32_t *t = reinterpret_cast<uint32_t *>(o.t_img + (e0 + le) * (int64_t)FROW);
+#pragma unroll 1
+                for (int k = 10 * q; k < min(10 * q + 10, FROW / 4); k++) t[k] = fr[k];
+            }
+        } else {
             const int le = tid >> 2, q = tid & 3;
             if (le < ne && s_term[le]) {
                 const uint8_t *fr = s_stk + le * FSTRIDE + FOFF;
@@ -818,7 +835,9 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         const int le = tid >> 2, q = tid & 3;
         if (le < ne) {
             const bool pop = s_popf[le];
-            render13(pop ? s_pgrid : s_grid, S, le, q, pop ? s_rp2[le] : s_rp[le], s_stk + le * FSTRIDE + FOFF);
+            const uint32_t rp = pop ? s_rp2[le] : s_rp[le];
+            render13(pop ? s_pgrid : s_grid, S, le, q, rp, s_stk + le * FSTRIDE + FOFF);
+            if (COMPACT && q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);   // row byte 0: direction
         }
     }
     __syncthreads();
@@ -832,7 +851,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     const int nd = s_nd;
     // ---- phase 2d (staged path): the older slots of each written terminal_observation
     // (the fast path writes them in phase 3 from registers)
-    if (s_tmask && !fast) {
+    if (s_tmask && !fast && !COMPACT) {
         const int le = tid >> 2, q = tid & 3;
         if (le < ne && s_term[le]) {
             uint8_t *t = o.t_img + (e0 + le) * (int64_t)IMG;
@@ -859,7 +878,16 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // Every quad is stored once, here: an earlier version stored the rows' old part right
     // after phase 1 and the rest here, so the 128-B lines across each row's seam were written
     // in two halves far apart in time; on MI355X that took 36 us per step instead of 27.
-    if (fast) {
+    if (COMPACT) {
+        // the block's rows are contiguous in LDS and in the output: one coalesced copy
+        const int nb16 = (ne * FROW) >> 4;
+        const uint4 *src = reinterpret_cast<const uint4 *>(s_stk);
+        uint4 *dst = reinterpret_cast<uint4 *>(o.img + e0 * (int64_t)FROW);
+        for (int i = tid; i < nb16; i += BLOCK_THREADS) dst[i] = src[i];
+        const int rem = ((ne * FROW) >> 2) - (nb16 << 2);          // trailing dwords (partial block)
+        if (tid < rem)
+            reinterpret_cast<uint32_t *>(dst + nb16)[tid] = reinterpret_cast<const uint32_t *>(src + nb16)[tid];
+    } else if (fast) {
         // Block-relative output dword k needs old dwords k+36, k+37 (alignbyte by 3) while its
         // env column j = k mod 147 <= 109; dword 110 mixes old byte 587 with new bytes 0..2;
         // dwords >= 111 are new-frame dwords (the LDS frame row holds new byte b at byte 1+b).
@@ -1238,6 +1266,141 @@ __global__ __launch_bounds__(256) void mgx_gae_kernel(const float *__restrict__ 
     }
 }
 
+// ========================================================= compact layout kernels
+// mgx_observe_compact: the current observation of every env as a compact row (byte 0
+// direction, bytes 1..147 the [c][vx][vy] frame) + mission id -- e.g. right after mgx_reset,
+// the first row of a compact rollout buffer.  One env per lane, from the engine state.
+__global__ __launch_bounds__(256) void mgx_observe_kernel(KParams p, uint8_t *__restrict__ rows, uint8_t *__restrict__ mids) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= p.n) return;
+    const EnvState st = p.state[e];
+    uint8_t *row = rows + e * (int64_t)FROW;
+    render_view(p.grid + e * p.GS, p.S, st.ax, st.ay, st.dir, st.carry, [&](int k, uint32_t v) {
+        row[1 + k] = (uint8_t)v;
+        row[1 + 49 + k] = (uint8_t)(v >> 8);
+        row[1 + 98 + k] = (uint8_t)(v >> 16);
+    });
+    if (p.vis) apply_vis(row + 1);                 // this thread's own global writes: read back coherently
+    row[0] = st.dir;
+    mids[e] = st.mission_id;
+}
+
+// mgx_gather: SB3 stacked observations (VecTransposeImage + VecFrameStack(n_stack)) rebuilt
+// from compact rows.  Sample b's newest frame is row index[b] (flat row*N + env) -- or, with
+// `newest` (terminal rows [N][148]), env's terminal row, the older frames then starting at
+// row index[b] itself.  Older slot k (1 <= k < n_stack) holds the row k steps back while no
+// episode start lies in between (starts[row] = 1: that row is an episode's first
+// observation), else zeros -- VecFrameStack's reset zeroing.  Outputs per sample: image
+// [3*n_stack][7][7] (u8, or f32 = u8 / 255 as SB3 preprocess_obs), direction one-hot
+// [4*n_stack] (u8 or f32), mission tokens [32*n_stack] (u8).  f32 = u8 * (1/255 in fp32): what
+// torch's `x.float() / 255.0` computes on the GPU (division by a scalar as a reciprocal multiply).
+// One workgroup per GATHER_TILE samples: phase A stages every needed row in LDS (dword loads,
+// coalesced along a row; rows are 148 B = 37 dwords), phase B writes the tile's outputs,
+// which are contiguous in memory, with consecutive threads on consecutive dwords.
+constexpr int GATHER_TILE = 16;
+constexpr int GATHER_MAXK = 8;
+__global__ __launch_bounds__(256) void mgx_gather_kernel(const uint8_t *__restrict__ rows, const uint8_t *__restrict__ mids,
+                                                         const uint8_t *__restrict__ starts, int64_t N, int K,
+                                                         const int64_t *__restrict__ index, int64_t B,
+                                                         const uint8_t *__restrict__ newest,
+                                                         const uint8_t *__restrict__ mtok, void *__restrict__ img_out,
+                                                         int img_f32, void *__restrict__ dir_out, int dir_f32,
+                                                         uint8_t *__restrict__ mis_out) {
+    __shared__ uint32_t s_row[GATHER_TILE * GATHER_MAXK * (FROW / 4)];   // zeros where the slot is empty
+    __shared__ int s_mid[GATHER_TILE * GATHER_MAXK];                     // -1: empty slot
+    const int tid = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * GATHER_TILE;
+    const int nb = (int)min<int64_t>(GATHER_TILE, B - b0);
+    const int npair = nb * K;
+    // phase A1: per (sample, slot): source row and validity
+    __shared__ const uint8_t *s_src[GATHER_TILE * GATHER_MAXK];
+    if (tid < npair) {
+        const int bi = tid / K, k = tid - bi * K;                        // k = slot (K-1 = newest)
+        const int64_t idx = index[b0 + bi];
+        const int64_t env = idx % N;
+        const int back = K - 1 - k;                                      // steps back from the newest
+        const uint8_t *src = nullptr;
+        int mid = -1;
+        if (newest) {
+            // newest = terminal row; older slot j back = row idx - (j-1)*N, valid while no start
+            // among rows idx .. idx - (j-2)*N (the terminal row itself continues the episode)
+            if (back == 0) { src = newest + env * FROW; mid = mids[idx]; }
+            else {
+                bool ok = true;
+                for (int j = 0; j < back - 1 && ok; j++) ok = !starts[idx - (int64_t)j * N];
+                if (ok) { const int64_t r = idx - (int64_t)(back - 1) * N; src = rows + r * FROW; mid = mids[r]; }
+            }
+        } else {
+            bool ok = true;
+            for (int j = 0; j < back && ok; j++) ok = !starts[idx - (int64_t)j * N];
+            if (ok) { const int64_t r = idx - (int64_t)back * N; src = rows + r * FROW; mid = mids[r]; }
+        }
+        s_src[tid] = src;
+        s_mid[tid] = mid;
+    }
+    __syncthreads();
+    // phase A2: stage the rows (37 dwords each)
+    constexpr int RW = FROW / 4;
+    for (int i = tid; i < npair * RW; i += blockDim.x) {
+        const int pr = i / RW, w = i - pr * RW;
+        const uint8_t *src = s_src[pr];
+        s_row[pr * RW + w] = src ? reinterpret_cast<const uint32_t *>(src)[w] : 0u;
+    }
+    __syncthreads();
+    const uint8_t *s_b = reinterpret_cast<const uint8_t *>(s_row);
+    // phase B1: images -- sample bi, output byte o = slot o / 147, frame byte o % 147 (row byte 1 + ...)
+    const int IMGB = FRAME * K;
+    const int nbytes = nb * IMGB;
+    if (img_f32) {
+        float4 *out = reinterpret_cast<float4 *>(static_cast<float *>(img_out) + b0 * IMGB);
+        for (int q = tid; q < (nbytes >> 2); q += blockDim.x) {
+            float v[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int o = 4 * q + t, bi = o / IMGB, ob = o - bi * IMGB, k = ob / FRAME, f = ob - k * FRAME;
+                v[t] = (float)s_b[(bi * K + k) * FROW + 1 + f] * (1.0f / 255.0f);
+            }
+            out[q] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+        for (int o = (nbytes & ~3) + tid; o < nbytes; o += blockDim.x) {
+            const int bi = o / IMGB, ob = o - bi * IMGB, k = ob / FRAME, f = ob - k * FRAME;
+            static_cast<float *>(img_out)[b0 * IMGB + o] = (float)s_b[(bi * K + k) * FROW + 1 + f] * (1.0f / 255.0f);
+        }
+    } else {
+        uint8_t *out = static_cast<uint8_t *>(img_out) + b0 * IMGB;
+        // the tile's output is 4-B aligned when IMGB is (n_stack multiple of 4: whole dwords)
+        const bool al = ((b0 * IMGB) & 3) == 0;
+        for (int q = tid; q < (nbytes >> 2); q += blockDim.x) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int o = 4 * q + t, bi = o / IMGB, ob = o - bi * IMGB, k = ob / FRAME, f = ob - k * FRAME;
+                w |= (uint32_t)s_b[(bi * K + k) * FROW + 1 + f] << (8 * t);
+            }
+            if (al) reinterpret_cast<uint32_t *>(out)[q] = w;
+            else for (int t = 0; t < 4; t++) out[4 * q + t] = (uint8_t)(w >> (8 * t));
+        }
+        for (int o = (nbytes & ~3) + tid; o < nbytes; o += blockDim.x) {
+            const int bi = o / IMGB, ob = o - bi * IMGB, k = ob / FRAME, f = ob - k * FRAME;
+            out[o] = s_b[(bi * K + k) * FROW + 1 + f];
+        }
+    }
+    // phase B2: direction one-hot (slot k: 4 values) and mission tokens (slot k: 32 tokens)
+    for (int i = tid; i < npair * 4; i += blockDim.x) {
+        const int pr = i >> 2, c = i & 3;
+        const bool on = s_mid[pr] >= 0 && s_b[pr * FROW] == c;
+        const int64_t o = (b0 + pr / K) * (int64_t)(4 * K) + (pr % K) * 4 + c;
+        if (dir_f32) static_cast<float *>(dir_out)[o] = on ? 1.0f : 0.0f;
+        else static_cast<uint8_t *>(dir_out)[o] = on ? 1 : 0;
+    }
+    for (int i = tid; i < npair * 8; i += blockDim.x) {
+        const int pr = i >> 3, c = i & 7;                                // 8 dwords of 4 tokens
+        const int mid = s_mid[pr];
+        const uint32_t v = mid >= 0 ? reinterpret_cast<const uint32_t *>(mtok + mid * 32)[c] : 0u;
+        reinterpret_cast<uint32_t *>(mis_out + (b0 + pr / K) * (int64_t)(32 * K) + (pr % K) * 32)[c] = v;
+    }
+}
+
 // ================================================================== host side
 thread_local std::string g_last_error;
 
@@ -1550,7 +1713,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.stk_lds = (std::max(BLOCK_ENVS * IMG, scratch) + 15) & ~15;   // reset kernel: stack area doubles as scratch
     p.grid_lds = (BLOCK_ENVS * (GS + 4) + 15) & ~15;
     p.fast_roll = cfg->n_stack == 4;
-    p.stk_step = p.fast_roll ? (BLOCK_ENVS * FROW + 15) & ~15 : (BLOCK_ENVS * IMG + 15) & ~15;
+    // (the compact layout always uses [64][148] frame rows, also at n_stack 1)
+    p.stk_step = (std::max(BLOCK_ENVS * FROW, p.fast_roll ? 0 : BLOCK_ENVS * IMG) + 15) & ~15;
     p.problem = cfg->problem;
     p.cfg_mission = cfg->mission;
     p.num_objects = cfg->num_objects;
@@ -1596,8 +1760,10 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->lds_step = (size_t)p.stk_step + (size_t)BLOCK_ENVS * 2 * GS   // grids + popped grids (chunk-major)
                   + (size_t)BLOCK_ENVS * 7 * 16;                      // + popped header, 2x2 token halves, RNG snapshot
     h->lds_reset = (size_t)p.stk_lds + (size_t)p.grid_lds;
-    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
-    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
     h->ext = cfg->obstacles || cfg->problem == MGX_PROBLEM_FULL || cfg->problem == MGX_PROBLEM_DRP ||
              cfg->problem == MGX_PROBLEM_MOV;
@@ -1772,10 +1938,10 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
         if (fs != MGX_OK) return fs;
     }
     if (action_bytes == 4)
-        hipLaunchKernelGGL(mgx_step_kernel<int32_t>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
+        hipLaunchKernelGGL((mgx_step_kernel<int32_t, false>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
                            (hipStream_t)stream, h->kp, o, (const int32_t *)actions_dev);
     else if (action_bytes == 8)
-        hipLaunchKernelGGL(mgx_step_kernel<int64_t>, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
+        hipLaunchKernelGGL((mgx_step_kernel<int64_t, false>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
                            (hipStream_t)stream, h->kp, o, (const int64_t *)actions_dev);
     HIP_TRY(hipGetLastError());
     if (h->kp.D == 0) {   // no ring: every done env is generated inline, right after the step
@@ -1785,6 +1951,72 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
     }
     h->calls++;
     if (h->kp.D > 0 && h->calls % (uint64_t)h->refill_every == 0) return join_refill(h, stream);
+    return MGX_OK;
+}
+
+mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_bytes, const mgx_compact_out *out,
+                            void *stream) {
+    if (!h || !out || !actions_dev) return fail(MGX_ERR_INVALID, "mgx_step_compact: null argument");
+    if (!out->row_dev || !out->mission_id_dev || !out->reward_dev || !out->terminated_dev || !out->truncated_dev)
+        return fail(MGX_ERR_INVALID, "mgx_step_compact: missing output buffer");
+    if (h->kp.terminal_mode != MGX_TERMINAL_NONE && !out->terminal_row_dev)
+        return fail(MGX_ERR_INVALID, "mgx_step_compact: terminal_mode needs terminal_row_dev");
+    if (h->kp.D == 0) return fail(MGX_ERR_INVALID, "mgx_step_compact: needs the episode ring (ring_depth >= 0)");
+    if (action_bytes != 4 && action_bytes != 8) return fail(MGX_ERR_INVALID, "action_bytes must be 4 or 8");
+    KOut o;
+    std::memset(&o, 0, sizeof o);
+    o.img = out->row_dev;
+    o.mis = out->mission_id_dev;
+    o.t_img = out->terminal_row_dev;
+    o.reward = out->reward_dev;
+    o.reward64 = out->reward64_dev;
+    o.term = out->terminated_dev;
+    o.trunc = out->truncated_dev;
+    o.done = out->done_dev;
+    o.ep_ret = out->ep_return_dev;
+    o.ep_len = out->ep_len_dev;
+    o.livelock = out->livelock_dev;
+    const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
+    if (h->calls % (uint64_t)h->refill_every == 0) {
+        mgx_status fs = fork_refill(h, stream);
+        if (fs != MGX_OK) return fs;
+    }
+    if (action_bytes == 4)
+        hipLaunchKernelGGL((mgx_step_kernel<int32_t, true>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
+                           (hipStream_t)stream, h->kp, o, (const int32_t *)actions_dev);
+    else
+        hipLaunchKernelGGL((mgx_step_kernel<int64_t, true>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
+                           (hipStream_t)stream, h->kp, o, (const int64_t *)actions_dev);
+    HIP_TRY(hipGetLastError());
+    h->calls++;
+    if (h->calls % (uint64_t)h->refill_every == 0) return join_refill(h, stream);
+    return MGX_OK;
+}
+
+mgx_status mgx_observe_compact(mgx_handle *h, uint8_t *row_dev, uint8_t *mission_id_dev, void *stream) {
+    if (!h || !row_dev || !mission_id_dev) return fail(MGX_ERR_INVALID, "mgx_observe_compact: null argument");
+    const int64_t nblk = (h->kp.n + 255) / 256;
+    hipLaunchKernelGGL(mgx_observe_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, h->kp, row_dev,
+                       mission_id_dev);
+    HIP_TRY(hipGetLastError());
+    return MGX_OK;
+}
+
+mgx_status mgx_gather(const mgx_handle *h, const uint8_t *rows_dev, const uint8_t *mission_ids_dev,
+                      const uint8_t *starts_dev, int64_t n_envs, const int64_t *index_dev, int64_t n_samples,
+                      const uint8_t *terminal_rows_dev, void *image_dev, int image_f32, void *direction_dev,
+                      int direction_f32, uint8_t *mission_dev, void *stream) {
+    if (!h || !rows_dev || !mission_ids_dev || !starts_dev || !index_dev || !image_dev || !direction_dev ||
+        !mission_dev || n_envs <= 0 || n_samples < 0)
+        return fail(MGX_ERR_INVALID, "mgx_gather: bad argument");
+    const int K = h->kp.n_stack;
+    if (K > GATHER_MAXK) return fail(MGX_ERR_INVALID, "mgx_gather: n_stack > 8");
+    if (n_samples == 0) return MGX_OK;
+    const int64_t nblk = (n_samples + GATHER_TILE - 1) / GATHER_TILE;
+    hipLaunchKernelGGL(mgx_gather_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, rows_dev,
+                       mission_ids_dev, starts_dev, n_envs, K, index_dev, n_samples, terminal_rows_dev, h->kp.mtok,
+                       image_dev, image_f32, direction_dev, direction_f32, mission_dev);
+    HIP_TRY(hipGetLastError());
     return MGX_OK;
 }
 

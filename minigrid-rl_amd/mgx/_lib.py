@@ -23,7 +23,8 @@ DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unk
 
 # Every entry point include/mgx.h declares (checked by tests/test_abi.py).
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
-           "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_gae_dones", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text")
+           "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_gae_dones", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text",
+           "mgx_step_compact", "mgx_observe_compact", "mgx_gather")
 
 
 class MgxConfig(ctypes.Structure):
@@ -47,6 +48,15 @@ class MgxObs(ctypes.Structure):
 class MgxStepOut(ctypes.Structure):
     _fields_ = [
         ("obs", MgxObs), ("terminal", MgxObs),
+        ("reward_dev", ctypes.c_void_p), ("reward64_dev", ctypes.c_void_p),
+        ("terminated_dev", ctypes.c_void_p), ("truncated_dev", ctypes.c_void_p), ("done_dev", ctypes.c_void_p),
+        ("ep_return_dev", ctypes.c_void_p), ("ep_len_dev", ctypes.c_void_p), ("livelock_dev", ctypes.c_void_p),
+    ]
+
+
+class MgxCompactOut(ctypes.Structure):
+    _fields_ = [
+        ("row_dev", ctypes.c_void_p), ("mission_id_dev", ctypes.c_void_p), ("terminal_row_dev", ctypes.c_void_p),
         ("reward_dev", ctypes.c_void_p), ("reward64_dev", ctypes.c_void_p),
         ("terminated_dev", ctypes.c_void_p), ("truncated_dev", ctypes.c_void_p), ("done_dev", ctypes.c_void_p),
         ("ep_return_dev", ctypes.c_void_p), ("ep_len_dev", ctypes.c_void_p), ("livelock_dev", ctypes.c_void_p),
@@ -86,6 +96,9 @@ def load():
     L.mgx_debug_counters.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.mgx_dump_state.argtypes = [P, P] + [P] * 10
     L.mgx_mission_text.argtypes = [I, ctypes.c_char_p, ctypes.c_size_t]
+    L.mgx_step_compact.argtypes = [P, P, I, ctypes.POINTER(MgxCompactOut), P]
+    L.mgx_observe_compact.argtypes = [P, P, P, P]
+    L.mgx_gather.argtypes = [P, P, P, P, I64, P, I64, P, P, I, P, I, P, P]
     for name in EXPORTS:
         getattr(L, name).restype = getattr(L, name).restype or I
     if L.mgx_abi_version() != ABI_VERSION:

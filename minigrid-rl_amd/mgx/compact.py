@@ -1,0 +1,115 @@
+"""Compact rollout layout: the engine writes each observation as
+one 148-B row (direction + [c][vx][vy] frame) plus a mission-id byte straight into a
+[rows, N] device buffer (mgx_step_compact), and mgx_gather rebuilds SB3's stacked
+observation (VecTransposeImage + VecFrameStack(n_stack), src/ppo.py:124-126) for any set
+of (t, env) samples -- optionally already as the policy's float input (preprocess_obs).
+
+Per env-step the buffer holds 150 B instead of the stacked 588 + 16 + 128..1024 B, and no
+stack is rolled per step.  Row layout of a rollout of T steps with H = n_stack - 1 history
+rows (the previous rollout's last observations):
+
+    row H + t   observation t (t = 0..T; row H + T is the observation after the last step)
+    starts[r]   1 if row r is an episode's first observation (= `done` of the step before)
+
+so GAE's per-step dones are starts[H+1 : H+T+1] (mgx_gae_dones)."""
+import ctypes
+
+import torch
+
+from . import _lib
+from .engine import _ptr
+
+ROW = 148
+
+
+class CompactBuffer:
+    """Device rollout storage for T steps of an MgxEngine's N envs in the compact layout."""
+
+    def __init__(self, engine, T, device=None):
+        self.engine = engine
+        self.T, self.N, self.K = int(T), engine.n, engine.n_stack
+        self.H = self.K - 1
+        R = self.T + self.H + 1
+        dev = device or engine.device
+        u8 = dict(dtype=torch.uint8, device=dev)
+        self.rows = torch.zeros((R, self.N, ROW), **u8)
+        self.mids = torch.zeros((R, self.N), **u8)
+        self.starts = torch.ones((R, self.N), **u8)          # history rows: "start" blocks older frames
+        self.terminal_rows = torch.zeros((self.N, ROW), **u8)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.rewards = torch.zeros((self.T, self.N), **f32)
+        self.terminated = torch.zeros((self.T, self.N), **u8)
+        self.truncated = torch.zeros((self.T, self.N), **u8)
+        self._out = _lib.MgxCompactOut()
+        self._arange = torch.arange(self.N, device=dev, dtype=torch.int64)
+
+    def row(self, t):
+        """Buffer row of observation t."""
+        return self.H + t
+
+    @property
+    def dones(self):
+        """u8 [T, N]: done of step t (= start flag of observation t+1)."""
+        return self.starts[self.H + 1:self.H + 1 + self.T]
+
+    def observe(self, t=0):
+        """Write every env's current observation as observation t (after a reset), start = 1."""
+        r = self.row(t)
+        e = self.engine
+        _lib.check(e.L.mgx_observe_compact(e.h, _ptr(self.rows[r]), _ptr(self.mids[r]), e._stream()),
+                   "mgx_observe_compact")
+        self.starts[r].fill_(1)
+
+    def step(self, t, actions):
+        """Step every env with `actions`; the new observation becomes observation t+1."""
+        e = self.engine
+        if actions.device != e.device or actions.dtype not in (torch.int32, torch.int64) \
+                or actions.shape != (self.N,) or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous int32/int64 [%d] tensor on %s" % (self.N, e.device))
+        r = self.row(t + 1)
+        o = self._out
+        o.row_dev = self.rows[r].data_ptr()
+        o.mission_id_dev = self.mids[r].data_ptr()
+        o.terminal_row_dev = self.terminal_rows.data_ptr()
+        o.reward_dev = self.rewards[t].data_ptr()
+        o.reward64_dev = None if e.reward64 is None else e.reward64.data_ptr()
+        o.terminated_dev = self.terminated[t].data_ptr()
+        o.truncated_dev = self.truncated[t].data_ptr()
+        o.done_dev = self.starts[r].data_ptr()
+        o.ep_return_dev = e.ep_return.data_ptr()
+        o.ep_len_dev = e.ep_len.data_ptr()
+        o.livelock_dev = e.livelock.data_ptr()
+        _lib.check(e.L.mgx_step_compact(e.h, _ptr(actions), actions.element_size(), ctypes.byref(o), e._stream()),
+                   "mgx_step_compact")
+        e.calls += 1
+
+    def carry_over(self):
+        """Start the next rollout: its history rows and observation 0 are this one's last rows."""
+        src = slice(self.T, self.T + self.H + 1)
+        for a in (self.rows, self.mids, self.starts):
+            a[:self.H + 1].copy_(a[src].clone() if self.T < self.H + 1 else a[src])
+
+    def gather(self, index, terminal=False, f32=True, out=None):
+        """Stacked observations of flat buffer indices `index` (i64 [B] = row * N + env):
+        dict(image [B, 3K, 7, 7], direction [B, 4K] (f32 = policy input, else u8), mission u8 [B, 32K]).
+        terminal=True: the stacked terminal_observation of the step that left row index."""
+        e = self.engine
+        B = index.numel()
+        K = self.K
+        if out is None:
+            ft = torch.float32 if f32 else torch.uint8
+            out = dict(image=torch.empty((B, 3 * K, 7, 7), dtype=ft, device=e.device),
+                       direction=torch.empty((B, 4 * K), dtype=ft, device=e.device),
+                       mission=torch.empty((B, 32 * K), dtype=torch.uint8, device=e.device))
+        idx = index.to(torch.int64).contiguous()
+        _lib.check(e.L.mgx_gather(e.h, _ptr(self.rows), _ptr(self.mids), _ptr(self.starts), self.N, _ptr(idx), B,
+                                  _ptr(self.terminal_rows) if terminal else None,
+                                  _ptr(out["image"]), int(out["image"].dtype == torch.float32),
+                                  _ptr(out["direction"]), int(out["direction"].dtype == torch.float32),
+                                  _ptr(out["mission"]), e._stream()), "mgx_gather")
+        return out
+
+    def gather_step(self, t, terminal=False, f32=True, out=None, envs=None):
+        """Stacked observation t of every env (or of `envs`)."""
+        ix = self._arange if envs is None else envs.to(torch.int64)
+        return self.gather(self.row(t) * self.N + ix, terminal=terminal, f32=f32, out=out)

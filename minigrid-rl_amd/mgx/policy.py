@@ -166,9 +166,11 @@ def _init_weights(module, gain=1.0):
 
 
 def preprocess(obs):
-    """SB3 preprocess_obs for the Dict space: image /255, the rest float."""
-    return {"image": obs["image"].float() / 255.0, "direction": obs["direction"].float(),
-            "mission": obs["mission"]}
+    """SB3 preprocess_obs for the Dict space: image /255, the rest float.  Float inputs are taken
+    as already preprocessed (mgx_gather's f32 output is exactly this, computed in the gather)."""
+    img = obs["image"]
+    return {"image": img if img.is_floating_point() else img.float() / 255.0,
+            "direction": obs["direction"].float(), "mission": obs["mission"]}
 
 
 class ActorCriticPolicy(nn.Module):

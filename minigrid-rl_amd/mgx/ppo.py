@@ -36,7 +36,8 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from .engine import MgxEngine, gae
+from .compact import CompactBuffer
+from .engine import MgxEngine, gae, gae_dones
 
 
 @dataclass
@@ -62,6 +63,7 @@ class PPOConfig:
     seed: int = 42
     adv_norm: str = "minibatch"         # "minibatch" (reference) | "global" (all-reduced stats)
     mission_cache: bool = True          # policy.py: GRU once per distinct mission stack
+    layout: str = "compact"             # rollout storage: "compact" (mgx/compact.py) | "sb3" (stacked obs)
     env: dict = field(default_factory=lambda: dict(problem="multi", mission=2, size=8, num_objects=4))
 
 
@@ -178,6 +180,105 @@ class RolloutCollector:
         return buf
 
 
+class CompactRollout:
+    """The rollout of CompactRolloutCollector: observations in the compact layout (one 148-B row
+    + mission id per env-step, stacks rebuilt by mgx_gather), per-step policy outputs, GAE."""
+
+    def __init__(self, engine, T):
+        self.buf = CompactBuffer(engine, T)
+        self.T, self.N = T, engine.n
+        dev = engine.device
+        self.actions = torch.zeros((T, self.N), dtype=torch.int64, device=dev)
+        self.values = torch.zeros((T, self.N), dtype=torch.float32, device=dev)
+        self.log_probs = torch.zeros((T, self.N), dtype=torch.float32, device=dev)
+        self.advantages = torch.zeros((T, self.N), dtype=torch.float32, device=dev)
+        self.returns = torch.zeros((T, self.N), dtype=torch.float32, device=dev)
+        self.adv_stats = torch.zeros(3, dtype=torch.float64, device=dev)
+
+    @property
+    def rewards(self):
+        return self.buf.rewards
+
+    def compute_returns_and_advantage(self, last_values, gamma, gae_lambda):
+        """SB3 GAE over the compact dones (mgx_gae_dones: next_non_terminal(t) = 1 - done(t))."""
+        self.adv_stats.zero_()
+        gae_dones(self.buf.rewards, self.values, self.buf.dones, last_values, gamma, gae_lambda,
+                  stats=self.adv_stats, out=(self.advantages, self.returns))
+
+    def minibatches(self, batch_size, perm):
+        """perm: permutation of the env-major flat index i = env * T + t (SB3 swap_and_flatten);
+        observations gathered straight into the policy's f32 input."""
+        T, N, H = self.T, self.N, self.buf.H
+        for s in range(0, perm.numel(), batch_size):
+            idx = perm[s:s + batch_size]
+            env, t = idx // T, idx % T
+            obs = self.buf.gather((H + t) * N + env, f32=True)
+            yield (obs, self.actions[t, env], self.values[t, env], self.log_probs[t, env],
+                   self.advantages[t, env], self.returns[t, env])
+
+
+class CompactRolloutCollector:
+    """OnPolicyAlgorithm.collect_rollouts over an MgxEngine with the compact layout: per step one
+    gather builds the policy's f32 input (VecFrameStack + preprocess_obs fused), one
+    mgx_step_compact writes the next observation row, reward and done straight into the rollout
+    buffer (no stack roll, no buffer copy)."""
+
+    def __init__(self, engine, policy, cfg):
+        self.engine, self.policy, self.cfg = engine, policy, cfg
+        self.rollout = CompactRollout(engine, cfg.horizon)
+        self.num_timesteps = 0
+        self.ep_returns, self.ep_lens = [], []
+        self.stopped = False
+        self._n_rollouts = 0
+        n, k, dev = engine.n, engine.n_stack, engine.device
+        self._obs = dict(image=torch.empty((n, 3 * k, 7, 7), dtype=torch.float32, device=dev),
+                         direction=torch.empty((n, 4 * k), dtype=torch.float32, device=dev),
+                         mission=torch.empty((n, 32 * k), dtype=torch.uint8, device=dev))
+
+    def start(self):
+        self.engine.reset()
+        self.rollout.buf.observe(0)
+        self._n_rollouts = 0
+
+    @torch.no_grad()
+    def collect(self, callback=None):
+        e, pol, cfg, ro = self.engine, self.policy, self.cfg, self.rollout
+        buf = ro.buf
+        if self._n_rollouts:
+            buf.carry_over()
+        self._n_rollouts += 1
+        pol.train(False)
+        gamma32 = torch.tensor(cfg.gamma, dtype=torch.float32)
+        ep_r, ep_l = [], []
+        for t in range(cfg.horizon):
+            obs = buf.gather_step(t, f32=True, out=self._obs)
+            actions, values, log_probs = pol(obs)
+            buf.step(t, actions)
+            self.num_timesteps += e.n
+            boot = (buf.truncated[t].bool() & ~buf.terminated[t].bool()).nonzero().flatten()
+            if boot.numel():
+                tv = pol.predict_values(buf.gather_step(t, terminal=True, envs=boot))
+                r = buf.rewards[t]
+                r.index_put_((boot,), r.index_select(0, boot) + gamma32.to(tv.device) * tv)
+            ro.actions[t].copy_(actions)
+            ro.values[t].copy_(values)
+            ro.log_probs[t].copy_(log_probs)
+            d = buf.dones[t].bool()
+            ep_r.append(torch.where(d, e.ep_return, torch.nan))
+            ep_l.append(torch.where(d, e.ep_len.float(), torch.nan))
+            if callback is not None:
+                if callback.on_step(pol, self.num_timesteps) is False:
+                    self.stopped = True
+                    return None
+                pol.train(False)
+        last_values = pol.predict_values(buf.gather_step(cfg.horizon, f32=True, out=self._obs))
+        ro.compute_returns_and_advantage(last_values, cfg.gamma, cfg.gae_lambda)
+        r, l = torch.stack(ep_r), torch.stack(ep_l)
+        m = ~torch.isnan(r)
+        self.ep_returns, self.ep_lens = r[m], l[m]
+        return ro
+
+
 class Trainer:
     """PPO.train (SB3) + the learn() loop; optional data-parallel group."""
 
@@ -254,6 +355,15 @@ class Trainer:
         return {k: float(torch.stack(v).mean()) for k, v in stats.items()} | {"lr": lr}
 
 
+def make_collector(engine, policy, cfg):
+    """The rollout collector of cfg.layout ("compact": CompactRolloutCollector, "sb3": RolloutCollector)."""
+    if cfg.layout == "compact":
+        return CompactRolloutCollector(engine, policy, cfg)
+    if cfg.layout == "sb3":
+        return RolloutCollector(engine, policy, cfg)
+    raise ValueError("layout must be 'compact' or 'sb3'")
+
+
 def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None, callback=None, evaluate=False):
     """PPO(...).learn(total_timesteps, callback=callback) for one rank's env shard; returns
     (policy, history, engine).  evaluate=True then runs evaluate_policy(model, vec_env,
@@ -269,7 +379,7 @@ def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None, cal
     if group is not None:   # identical initial weights on every rank
         for p in pol.parameters():
             torch.distributed.broadcast(p.data, 0, group=group)
-    col = RolloutCollector(eng, pol, cfg)
+    col = make_collector(eng, pol, cfg)
     tr = Trainer(pol, cfg, group)
     col.start()
     hist = []

@@ -1,0 +1,109 @@
+"""Compact rollout layout (mgx_step_compact + mgx_gather, mgx/compact.py) against the SB3
+layout the engine materialises (mgx_step): two engines of the same config and seed stepped in
+lockstep; every step, the stacked observation and the stacked terminal_observation rebuilt by
+the gather kernel must equal the engine's materialised stacks bit for bit (which are pinned to
+the reference fixtures by test_gpu_parity.py), and the f32 gather must equal torch's
+preprocess_obs of them (image / 255 on the same device)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+CASES = [dict(problem="multi", mission=None, size=8, n=200, n_stack=4),
+         dict(problem="multi", mission=1, size=16, n=130, n_stack=4, see_through_walls=False),
+         dict(problem="multi", mission=2, size=11, n=77, n_stack=3, all_doors_open=True),
+         dict(problem="pkp", mission=None, size=8, n=64, n_stack=1)]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "%s_%s_s%d_n%d_k%d" % (
+    c["problem"], c["mission"], c["size"], c["n"], c["n_stack"]))
+def test_gathered_stacks_equal_materialised_stacks(case):
+    _need_gpu()
+    from mgx import MgxEngine
+    from mgx.compact import CompactBuffer
+    from mgx.policy import preprocess
+    kw = dict(case)
+    n, k = kw.pop("n"), kw.pop("n_stack")
+    T = 96
+    ref = MgxEngine(n_envs=n, n_stack=k, terminal_mode="all", mission_dtype=torch.uint8, reward64=True, **kw)
+    cmp_ = MgxEngine(n_envs=n, n_stack=k, terminal_mode="all", mission_dtype=torch.uint8, reward64=True, **kw)
+    buf = CompactBuffer(cmp_, T)
+    obs = ref.reset()
+    cmp_.reset()
+    buf.observe(0)
+    g = buf.gather_step(0, f32=False)
+    for key in ("image", "direction", "mission"):
+        assert torch.equal(g[key], obs[key]), key
+    rng = np.random.default_rng(11)
+    n_done = 0
+    for t in range(T):
+        # bursts of 'done' make episodes start inside every stack position
+        a = np.full(n, 6) if t % 23 == 5 else rng.integers(0, 7, n)
+        act = torch.as_tensor(a, device=ref.device)
+        obs = ref.step(act)
+        buf.step(t, act)
+        assert torch.equal(buf.rewards[t], ref.reward), t
+        assert torch.equal(buf.dones[t].bool(), ref.done), t
+        assert torch.equal(buf.terminated[t].bool(), ref.terminated), t
+        g = buf.gather_step(t + 1, f32=False)
+        for key in ("image", "direction", "mission"):
+            assert torch.equal(g[key], obs[key]), (t, key)
+        d = ref.done.nonzero().flatten()
+        if d.numel():
+            n_done += d.numel()
+            gt = buf.gather_step(t, terminal=True, f32=False, envs=d)
+            for key in ("image", "direction", "mission"):
+                assert torch.equal(gt[key], ref.terminal_obs[key][d]), (t, key)
+        if t % 16 == 0:
+            gf = buf.gather_step(t + 1, f32=True)
+            want = preprocess(obs)
+            assert torch.equal(gf["image"], want["image"]), t
+            assert torch.equal(gf["direction"], want["direction"]), t
+    assert n_done > n
+    ref.poll_error()
+    cmp_.poll_error()
+    a_, b_ = ref.dump_state(), cmp_.dump_state()
+    for key in ("grid", "agent", "mtwords", "pcg"):
+        assert np.array_equal(a_[key], b_[key]), key
+
+
+def test_carry_over_and_minibatch_gather():
+    """Two rollouts of T=8 with the buffer carried over: any (t, env) sample of the second
+    rollout, in a random minibatch order, gathers the stack the SB3 engine showed at that step
+    (the history rows bridge the rollout boundary)."""
+    _need_gpu()
+    from mgx import MgxEngine
+    from mgx.compact import CompactBuffer
+    n, T = 96, 8
+    ref = MgxEngine(problem="multi", mission=None, size=8, n_envs=n, mission_dtype=torch.uint8)
+    cmp_ = MgxEngine(problem="multi", mission=None, size=8, n_envs=n, mission_dtype=torch.uint8)
+    buf = CompactBuffer(cmp_, T)
+    ref.reset()
+    cmp_.reset()
+    buf.observe(0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    for roll in range(2):
+        seen = []
+        for t in range(T):
+            seen.append({k: v.clone() for k, v in ref.obs.items()})
+            a = torch.randint(0, 7, (n,), device="cuda", generator=g)
+            ref.step(a)
+            buf.step(t, a)
+        if roll == 0:
+            buf.carry_over()
+            continue
+        perm = torch.randperm(n * T, device="cuda")            # env-major flat index (swap_and_flatten)
+        env, t_ = perm // T, perm % T
+        got = buf.gather((buf.H + t_) * n + env, f32=False)
+        for key in ("image", "direction", "mission"):
+            want = torch.stack([seen[int(tt)][key][int(ee)] for tt, ee in zip(t_.tolist(), env.tolist())])
+            assert torch.equal(got[key], want), key

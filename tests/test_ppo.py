@@ -219,15 +219,20 @@ def test_data_parallel_gloo_world2():
 
 # ------------------------------------------------------------------------ GPU
 @pytest.mark.gpu
-def test_rollout_collector_matches_sb3_loop():
+@pytest.mark.parametrize("env_kw,T", [(dict(problem="gtg", mission=5, size=6, num_objects=2), 48),
+                                      (dict(problem="multi", mission=2, size=8, num_objects=4), 80)],
+                         ids=["gtg6", "pkp8_config3"])
+def test_rollout_collector_matches_sb3_loop(env_kw, T):
+    """The device-resident collector (SB3 stacked layout) against SB3's collect_rollouts loop
+    driven through the MgxVecEnv drop-in, on a small single-room case and on BASELINE config
+    3's workload (multi / 'pick up' / 8x8; T=80 > max_steps so truncation bootstraps occur)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import oracle as O
     from mgx import MgxEngine, MgxVecEnv
     from mgx.ppo import RolloutCollector
-    n, T = 96, 48
-    env_kw = dict(problem="gtg", mission=5, size=6, num_objects=2)
-    cfg = PPOConfig(n_envs=n, horizon=T, env=env_kw)
+    n = 96
+    cfg = PPOConfig(n_envs=n, horizon=T, env=env_kw, layout="sb3")
     torch.manual_seed(0)
     pol = ActorCriticPolicy().cuda()
     with torch.no_grad():
@@ -274,6 +279,53 @@ def test_rollout_collector_matches_sb3_loop():
     np.testing.assert_allclose(buf.advantages.cpu().numpy(), want_a, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(buf.returns.cpu().numpy(), want_r, rtol=1e-5, atol=1e-5)
     eng.poll_error()
+
+
+@pytest.mark.gpu
+def test_compact_collector_equals_sb3_layout_collector():
+    """CompactRolloutCollector (compact rows + mgx_gather into the policy's f32 input +
+    mgx_gae_dones) against RolloutCollector (materialised SB3 stacks + mgx_gae) on config 3's
+    workload, two rollouts (the second starts from carried-over history rows): same policy,
+    same torch RNG -> the same actions, values, rewards (with truncation bootstraps), advantages
+    and returns; then one PPO update from each buffer gives the same weights (minibatches
+    gathered vs indexed)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mgx import MgxEngine
+    from mgx.ppo import CompactRolloutCollector, RolloutCollector
+    n, T = 256, 72
+    env_kw = dict(problem="multi", mission=2, size=8, num_objects=4)
+    torch.manual_seed(0)
+    pol_a = ActorCriticPolicy().cuda()
+    with torch.no_grad():
+        pol_a.action_net.bias[6] = -30.0                     # rarely 'done': truncations happen
+    pol_b = copy.deepcopy(pol_a)
+    pol_b.optimizer = torch.optim.Adam(pol_b.parameters(), lr=3e-4, eps=1e-8)
+    pol_b.optimizer.load_state_dict(pol_a.optimizer.state_dict())
+    mk = lambda: MgxEngine(n_envs=n, n_stack=4, terminal_mode="truncated", mission_dtype=torch.uint8,  # noqa: E731
+                           **env_kw)
+    ca = RolloutCollector(mk(), pol_a, PPOConfig(n_envs=n, horizon=T, env=env_kw, layout="sb3"))
+    cb = CompactRolloutCollector(mk(), pol_b, PPOConfig(n_envs=n, horizon=T, env=env_kw))
+    ca.start()
+    cb.start()
+    for roll in range(2):
+        torch.manual_seed(77 + roll)
+        ba = ca.collect()
+        torch.manual_seed(77 + roll)
+        bb = cb.collect()
+        assert torch.equal(ba.actions, bb.actions), roll
+        assert torch.equal(ba.values, bb.values), roll
+        assert torch.equal(ba.episode_starts[1:], bb.buf.dones[:-1].float()), roll
+        assert bool((bb.buf.truncated.bool() & ~bb.buf.terminated.bool()).any())
+        torch.testing.assert_close(ba.rewards, bb.rewards, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(ba.advantages, bb.advantages, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(ba.returns, bb.returns, rtol=1e-5, atol=1e-5)
+    cfg = PPOConfig(n_envs=n, horizon=T, batch_size=4608, n_epochs=1)
+    perm = torch.randperm(n * T, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
+    Trainer(pol_a, cfg).train(ba, 1.0, perm_fn=lambda _: perm)
+    Trainer(pol_b, cfg).train(bb, 1.0, perm_fn=lambda _: perm)
+    for (name, a), (_, b) in zip(pol_a.named_parameters(), pol_b.named_parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=name)
 
 
 def test_conv2d_gemm_equals_conv2d():
