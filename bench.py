@@ -1,8 +1,13 @@
 """bench.py -- env-steps/s of the MI355X MiniGrid engine (BASELINE config 2).
 
-Workload (one "step" = one vectorised step of the whole per-GPU batch through
-the drop-in path: PlaygroundEnv.step + gen_obs + VecTransposeImage +
-VecFrameStack(4) roll + SubprocVecEnv auto-reset, i.e. one `mgx_step`):
+Workload (one "step" = one vectorised step of the whole per-GPU batch:
+PlaygroundEnv.step + gen_obs + the two wrappers + SubprocVecEnv auto-reset, the
+new observation written into the rollout buffer in the compact layout -- one
+148-B row + mission id per env (`mgx_step_compact`; the collector's stacked
+VecFrameStack(4) input is rebuilt from rows by `mgx_gather`, bit-exact with the
+materialised stacks, tests/test_compact.py).  At N=1 the same workload with the
+materialised SB3 stacks (`mgx_step`: VecTransposeImage + VecFrameStack roll per
+step, the MgxVecEnv drop-in) is timed too and reported as `sb3_layout`):
   multi / mission 5 ('go to goal', GTG) / 8x8 / num_objects 4 / 65,536 envs per
   GPU, uniform random actions on {0..6} (pre-generated on device for all
   warmup+timed steps, so inputs are resident in HBM), seed 42, env global
@@ -49,6 +54,7 @@ METRIC = "env-steps/sec at 65k parallel envs, 1/2/4/8 MI355X; % HBM roofline"
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_STEP = 334                    # per env-step algorithmic bytes
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+PMC_FILE_COMPACT = os.path.join(ROOT, "profiles", "pmc_step_kernel_compact.json")
 
 
 def parse():
@@ -76,8 +82,10 @@ def parse():
                          "largest whole-epoch divisor of --steps up to 1024; ppo: default 16)")
     ap.add_argument("--batch-size", type=int, default=65536, help="ppo: minibatch size")
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
-    ap.add_argument("--layout", default="compact", choices=["compact", "sb3"],
-                    help="ppo: rollout storage (compact rows + gather, or materialised SB3 stacks)")
+    ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layout")
+    ap.add_argument("--layout", default=None, choices=["compact", "sb3"],
+                    help="observation storage: materialised SB3 stacks (mgx_step; rollout default) or "
+                         "compact rows + mgx_gather (mgx_step_compact; ppo default)")
     args = ap.parse_args()
     presets = {2: dict(mission="5", size=8, n_envs=65536), 4: dict(mission="None", size=8, n_envs=32768),
                5: dict(mission="1", size=16, n_envs=131072)}
@@ -91,6 +99,8 @@ def parse():
         args.warmup = 1 if ppo else 128
     if ppo and args.horizon is None:
         args.horizon = 16
+    if args.layout is None:
+        args.layout = "compact"
     return args
 
 
@@ -318,31 +328,10 @@ def gae_probe(dev, n, T, reps=20):
             "frac": b / us / 1e3 / PEAK_HBM_GBPS, "unit": "GB/s"}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    cpu = None
-    if args.workload == "rollout" and args.cpu_seconds > 0 and world == 1:
-        cpu = cpu_baseline(args, args.cpu_seconds)      # before any GPU call (forks workers)
-    # one process per GPU; `local % device_count` only matters for a rehearsal of the
-    # N>1 path with more ranks than GPUs (MGX_DIST_BACKEND=gloo: RCCL refuses shared GPUs)
-    ndev = torch.cuda.device_count()
-    gpu = local % max(ndev, 1)
-    backend = os.environ.get("MGX_DIST_BACKEND", "nccl")
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(backend)
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    if args.workload == "ppo":
-        return main_ppo(args, world, rank, local, dev)
+def measure_rollout(args, layout, world, rank, dev):
+    """One rollout measurement (the timed region of the module docstring) on a fresh engine;
+    returns the JSON dict on rank 0."""
     from mgx import MgxEngine, gae_dones
-
     n = args.n_envs
     mission = None if args.mission == "None" else int(args.mission)
     K = args.steps
@@ -364,8 +353,17 @@ def main():
     # rollout storage the steps write directly (compact layout): reward f32 and done u8 per step;
     # values are synthetic (the rollout bench has no policy); GAE + the (sum A, sum A^2, n)
     # all-reduce run once per horizon inside the timed region
-    rew = torch.zeros((H, n), dtype=torch.float32, device=dev)
-    dones = torch.zeros((H, n), dtype=torch.uint8, device=dev)
+    compact = layout == "compact"
+    cbuf = None
+    if compact:
+        # compact layout: each step writes its observation row, reward and done straight into the
+        # rollout buffer (mgx_step_compact); GAE reads the buffer's rewards and dones
+        from mgx.compact import CompactBuffer
+        cbuf = CompactBuffer(eng, H)
+        rew, dones = cbuf.rewards, cbuf.dones
+    else:
+        rew = torch.zeros((H, n), dtype=torch.float32, device=dev)
+        dones = torch.zeros((H, n), dtype=torch.uint8, device=dev)
     vals = torch.randn((H, n), device=dev, generator=g)
     last_v = torch.randn(n, device=dev, generator=g)
     adv, ret = torch.empty_like(rew), torch.empty_like(rew)
@@ -373,15 +371,29 @@ def main():
     gamma, lam = 0.8108071290665859, 0.9452281119742252
     eng.reset()
     stream = torch.cuda.current_stream(dev)
-    for t in range(W):
-        eng.step(actions[t])
+    if compact:
+        cbuf.observe(0)
+        for t in range(W):
+            if t and t % H == 0:
+                cbuf.carry_over()
+            cbuf.step(t % H, actions[t])
+        cbuf.carry_over()
+    else:
+        for t in range(W):
+            eng.step(actions[t])
     torch.cuda.synchronize(dev)
     assert eng.calls % E == 0                            # the timed region starts on an epoch boundary
 
     def chunk(c):
         st.zero_()
-        for j in range(H):
-            eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
+        if compact:
+            if c:
+                cbuf.carry_over()
+            for j in range(H):
+                cbuf.step(j, actions[W + c * H + j])
+        else:
+            for j in range(H):
+                eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
         if not aligned and c == K // H - 1:
             eng.join()                                   # last epoch still forked: pay for all of it
         gae_dones(rew, vals, dones, last_v, gamma, lam, stats=st, out=(adv, ret))
@@ -434,18 +446,24 @@ def main():
     # bracketed by one event pair, so the per-launch figure is kernel time plus the
     # back-to-back dispatch gap (no host latency in it).
     windows, cur = [], None
+
+    def probe_step(t):
+        if compact:
+            cbuf.step(t % H, actions[W + K + t])   # rows are overwritten: timing only
+        else:
+            eng.step(actions[W + K + t])
     for t in range(P):
         if eng.epoch_boundary():
             if cur is not None:
                 cur[1].record(stream)
                 windows.append(cur)
                 cur = None
-            eng.step(actions[W + K + t])
+            probe_step(t)
             continue
         if cur is None:
             cur = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), 0]
             cur[0].record(stream)
-        eng.step(actions[W + K + t])
+        probe_step(t)
         cur[2] += 1
     if cur is not None:
         cur[1].record(stream)
@@ -474,14 +492,16 @@ def main():
         b_alg = B_STEP * n + (3 * args.size ** 2 + 208) * resets_per_launch
         achieved = b_alg / per_launch_s / 1e9
         traffic = None
-        if os.path.exists(PMC_FILE):
+        pmc_file = PMC_FILE_COMPACT if compact else PMC_FILE
+        if os.path.exists(pmc_file):
             try:
-                pmc = json.load(open(PMC_FILE))
+                pmc = json.load(open(pmc_file))
                 if pmc.get("n_envs") == n and pmc.get("size") == args.size and pmc.get("mission") == mission:
                     traffic = pmc.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
-        stack_bytes = n * (441 + 588 + 12 + 16)   # VecFrameStack image + direction roll (reported separately)
+        # VecFrameStack image + direction roll (reported separately); the compact layout rolls nothing
+        stack_bytes = 0 if compact else n * (441 + 588 + 12 + 16)
         out = {
             "metric": METRIC,
             "value": total_env_steps / wall_max,
@@ -497,10 +517,11 @@ def main():
             "dtype": "u8",
             "data": "synthetic (uniform random actions on {0..6}, seed 1234+rank; env i seeded 42+i; "
                     "synthetic values for GAE)",
-            "config": {"workload": _workload_name(args, mission, n, world),
+            "config": {"workload": _workload_name(args, mission, n, world) + (
+                           " [compact layout: observation rows into the rollout buffer]" if compact else ""),
                        "problem": args.problem, "mission": mission, "size": args.size, "num_objects": 4,
                        "envs_per_gpu": n, "n_stack": args.n_stack, "parallelism": "env-sharded dp%d" % world,
-                       "hipgraph": bool(graphs), "refill_every": E, "horizon": H,
+                       "hipgraph": bool(graphs), "refill_every": E, "horizon": H, "layout": layout,
                        "timed": "%d steps = %d whole refill epochs%s; GAE + adv-stat %s every %d steps" % (
                            K, K // E, "" if aligned else " + a joined partial one",
                            "all-reduce (%s)" % dist.get_backend() if world > 1 else "accumulation", H)},
@@ -510,7 +531,8 @@ def main():
                        "gae_launches": nchunks},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
-                         "kernel": "mgx_step_kernel", "avg_launch_us": per_launch_s * 1e6,
+                         "kernel": "mgx_step_kernel<int, %s>" % ("true> (compact" if compact else "false> (SB3 stacks"),
+                         "avg_launch_us": per_launch_s * 1e6,
                          "probe_launches": len(probe_us),
                          "step_pipeline_us": float(gpu_ms) * 1e3 / K,
                          "alg_bytes_per_launch": b_alg, "resets_per_launch": resets_per_launch,
@@ -519,6 +541,41 @@ def main():
             "gae": {"horizon": gae_h, "T1024": gae_1k},
             "gpu_time_ms": gpu_max * 1e3,
         }
+        return out
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if args.workload == "rollout" and args.cpu_seconds > 0 and world == 1:
+        cpu = cpu_baseline(args, args.cpu_seconds)      # before any GPU call (forks workers)
+    # one process per GPU; `local % device_count` only matters for a rehearsal of the
+    # N>1 path with more ranks than GPUs (MGX_DIST_BACKEND=gloo: RCCL refuses shared GPUs)
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)
+    backend = os.environ.get("MGX_DIST_BACKEND", "nccl")
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    if args.workload == "ppo":
+        return main_ppo(args, world, rank, local, dev)
+    out = measure_rollout(args, args.layout, world, rank, dev)
+    if world == 1 and args.both_layouts:
+        # the other observation layout on the same workload, reported beside the headline
+        other = "sb3" if args.layout == "compact" else "compact"
+        torch.cuda.empty_cache()
+        o2 = measure_rollout(args, other, world, rank, dev)
+        out[other + "_layout"] = {k: o2[k] for k in ("value", "ms_per_step", "roofline", "window")}
+    if rank == 0:
         if cpu is not None:
             out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)

@@ -1299,21 +1299,22 @@ __global__ __launch_bounds__(256) void mgx_observe_kernel(KParams p, uint8_t *__
 // which are contiguous in memory, with consecutive threads on consecutive dwords.
 constexpr int GATHER_TILE = 16;
 constexpr int GATHER_MAXK = 8;
+template <int K, bool F32>   // n_stack and output type are compile-time: every index split is a constant division
 __global__ __launch_bounds__(256) void mgx_gather_kernel(const uint8_t *__restrict__ rows, const uint8_t *__restrict__ mids,
-                                                         const uint8_t *__restrict__ starts, int64_t N, int K,
+                                                         const uint8_t *__restrict__ starts, int64_t N,
                                                          const int64_t *__restrict__ index, int64_t B,
                                                          const uint8_t *__restrict__ newest,
                                                          const uint8_t *__restrict__ mtok, void *__restrict__ img_out,
-                                                         int img_f32, void *__restrict__ dir_out, int dir_f32,
-                                                         uint8_t *__restrict__ mis_out) {
-    __shared__ uint32_t s_row[GATHER_TILE * GATHER_MAXK * (FROW / 4)];   // zeros where the slot is empty
-    __shared__ int s_mid[GATHER_TILE * GATHER_MAXK];                     // -1: empty slot
+                                                         void *__restrict__ dir_out, uint8_t *__restrict__ mis_out) {
+    constexpr int img_f32 = F32, dir_f32 = F32;
+    __shared__ uint32_t s_row[GATHER_TILE * K * (FROW / 4)];             // zeros where the slot is empty
+    __shared__ int s_mid[GATHER_TILE * K];                               // -1: empty slot
     const int tid = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * GATHER_TILE;
     const int nb = (int)min<int64_t>(GATHER_TILE, B - b0);
     const int npair = nb * K;
     // phase A1: per (sample, slot): source row and validity
-    __shared__ const uint8_t *s_src[GATHER_TILE * GATHER_MAXK];
+    __shared__ const uint8_t *s_src[GATHER_TILE * K];
     if (tid < npair) {
         const int bi = tid / K, k = tid - bi * K;                        // k = slot (K-1 = newest)
         const int64_t idx = index[b0 + bi];
@@ -1349,7 +1350,7 @@ __global__ __launch_bounds__(256) void mgx_gather_kernel(const uint8_t *__restri
     __syncthreads();
     const uint8_t *s_b = reinterpret_cast<const uint8_t *>(s_row);
     // phase B1: images -- sample bi, output byte o = slot o / 147, frame byte o % 147 (row byte 1 + ...)
-    const int IMGB = FRAME * K;
+    constexpr int IMGB = FRAME * K;
     const int nbytes = nb * IMGB;
     if (img_f32) {
         float4 *out = reinterpret_cast<float4 *>(static_cast<float *>(img_out) + b0 * IMGB);
@@ -2012,10 +2013,24 @@ mgx_status mgx_gather(const mgx_handle *h, const uint8_t *rows_dev, const uint8_
     const int K = h->kp.n_stack;
     if (K > GATHER_MAXK) return fail(MGX_ERR_INVALID, "mgx_gather: n_stack > 8");
     if (n_samples == 0) return MGX_OK;
+    if (!image_f32 != !direction_f32) return fail(MGX_ERR_INVALID, "mgx_gather: image and direction share one dtype");
     const int64_t nblk = (n_samples + GATHER_TILE - 1) / GATHER_TILE;
-    hipLaunchKernelGGL(mgx_gather_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, rows_dev,
-                       mission_ids_dev, starts_dev, n_envs, K, index_dev, n_samples, terminal_rows_dev, h->kp.mtok,
-                       image_dev, image_f32, direction_dev, direction_f32, mission_dev);
+#define MGX_GATHER(KK)                                                                                           \
+    case KK:                                                                                                     \
+        if (image_f32)                                                                                           \
+            hipLaunchKernelGGL((mgx_gather_kernel<KK, true>), dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, \
+                               rows_dev, mission_ids_dev, starts_dev, n_envs, index_dev, n_samples, terminal_rows_dev, \
+                               h->kp.mtok, image_dev, direction_dev, mission_dev);                              \
+        else                                                                                                     \
+            hipLaunchKernelGGL((mgx_gather_kernel<KK, false>), dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, \
+                               rows_dev, mission_ids_dev, starts_dev, n_envs, index_dev, n_samples, terminal_rows_dev, \
+                               h->kp.mtok, image_dev, direction_dev, mission_dev);                              \
+        break;
+    switch (K) {
+        MGX_GATHER(1) MGX_GATHER(2) MGX_GATHER(3) MGX_GATHER(4) MGX_GATHER(5) MGX_GATHER(6) MGX_GATHER(7) MGX_GATHER(8)
+        default: return fail(MGX_ERR_INVALID, "mgx_gather: n_stack out of range");
+    }
+#undef MGX_GATHER
     HIP_TRY(hipGetLastError());
     return MGX_OK;
 }
