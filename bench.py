@@ -343,9 +343,11 @@ def measure_rollout(args, layout, world, rank, dev):
                     refill_every=E or 0, refill_cap=args.refill_cap, ring_depth=args.ring_depth)
     E = eng.refill_every
     H = pick_horizon(K, E if aligned else None, args.horizon or 0)
-    # warm-up: whole refill epochs, and at least 128 steps -- the rings start at 2E episodes and
-    # fill towards D, so a shorter warm-up would time the fill-up, not the steady state
-    W = -(-max(args.warmup, 128) // E) * E
+    # warm-up: whole refill epochs, and at least 640 steps -- the rings start at 2E episodes and
+    # fill towards D (at most `refill_cap` per env per epoch beyond consumption); a shorter
+    # warm-up would time that fill-up (the refill producing ~2x what the steps consume), not the
+    # steady state, where production = consumption (`window` reports both)
+    W = -(-max(args.warmup, 640) // E) * E
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     P = args.probe
@@ -531,7 +533,7 @@ def measure_rollout(args, layout, world, rank, dev):
                        "gae_launches": nchunks},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
-                         "kernel": "mgx_step_kernel<int, %s>" % ("true> (compact" if compact else "false> (SB3 stacks"),
+                         "kernel": "mgx_step_kernel<int, %s>" % ("true> (compact)" if compact else "false> (SB3 stacks)"),
                          "avg_launch_us": per_launch_s * 1e6,
                          "probe_launches": len(probe_us),
                          "step_pipeline_us": float(gpu_ms) * 1e3 / K,

@@ -1178,90 +1178,124 @@ __global__ __launch_bounds__(64, 3) void mgx_refill_kernel<1, false>(KParams p) 
 // ================================================================ GAE kernel
 // DictRolloutBuffer.compute_returns_and_advantage (SB3; fp32, numpy op order,
 // built with -ffp-contract=off):  delta = ((r + (g*nv)*nnt) - V);  last = delta + (c*nnt)*last
-// The recurrence is serial in t and must round exactly like the sequential numpy loop, so
-// the only parallelism is one column (env) per lane.  Latency, not bandwidth, bounds a
-// naive walk (one dependent load round trip per t): the loads of the next GAE_U steps are
-// issued before the current GAE_U are computed (register double buffer), so each lane keeps
-// 3*GAE_U loads in flight.  DONES: the compact form -- `es` is u8 dones[T][N] (done after
-// step t), next_non_terminal(t) = 1 - dones[t]; otherwise SB3's f32 episode_starts[T][N]
-// plus last_dones (next_non_terminal(t) = 1 - episode_starts[t+1], 1 - last_dones at T-1).
-constexpr int GAE_U = 32;     // steps per chunk: 3*32 loads in flight per lane (one wave per SIMD at N=65,536)
+// One workgroup of 256 threads per 64 columns (envs).  The recurrence is serial in t and must
+// round exactly like the sequential numpy loop, so one wave (lane = column) computes it; the
+// other three waves only load.  Tiles of GAE_TT steps, walked from t = T-1 down: while wave 0
+// computes tile k from LDS (and stores adv/ret straight to HBM, coalesced), every thread already
+// has its share of tile k+1 in flight in registers (float4 loads), written to LDS after the
+// compute -- 64 x GAE_TT x 9 B per workgroup in flight, ~37 MB across the GPU at N = 65,536
+// (a lane-per-column walk keeps at most 63 loads per wave in flight: latency-bound).
+// DONES: the compact form -- `es` is u8 dones[T][N] (done after step t), next_non_terminal(t) =
+// 1 - dones[t]; otherwise SB3's f32 episode_starts[T][N] plus last_dones (next_non_terminal(t)
+// = 1 - episode_starts[t+1], 1 - last_dones at T-1).
+constexpr int GAE_TT = 64;                 // steps per tile
+typedef float gf4 __attribute__((ext_vector_type(4)));
 
 template <bool DONES>
-struct GaeChunk {
-    float r[GAE_U], v[GAE_U], e[GAE_U];
-};
-
-template <bool DONES>
-__device__ __forceinline__ void gae_load(GaeChunk<DONES> &c, const float *__restrict__ r, const float *__restrict__ v,
-                                         const void *__restrict__ es, int64_t t, int64_t N, int64_t i) {
-    // chunk = steps t, t-1, ..., t-GAE_U+1 (entries with t-j < 0 are never used).  For the f32
-    // form the flag loaded for step t-j is episode_starts[t-j] (used by step t-j-1).
-#pragma unroll
-    for (int j = 0; j < GAE_U; j++) {
-        const int64_t tt = t - j;
-        if (tt >= 0) {
-            const int64_t k = tt * N + i;
-            c.r[j] = __builtin_nontemporal_load(r + k);
-            c.v[j] = __builtin_nontemporal_load(v + k);
-            c.e[j] = DONES ? (float)__builtin_nontemporal_load(static_cast<const uint8_t *>(es) + k)
-                           : __builtin_nontemporal_load(static_cast<const float *>(es) + k);
-        }
-    }
-}
-
-template <bool DONES>
-__global__ __launch_bounds__(256) void mgx_gae_kernel(const float *__restrict__ r, const float *__restrict__ v,
+__global__ __launch_bounds__(256, 4) void mgx_gae_kernel(const float *__restrict__ r, const float *__restrict__ v,
                                                       const void *__restrict__ es, const float *__restrict__ lv,
                                                       const uint8_t *__restrict__ ld, int64_t T, int64_t N, float g,
                                                       float c, float *__restrict__ adv, float *__restrict__ ret,
                                                       double *__restrict__ stats) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    double s1 = 0.0, s2 = 0.0;
-    if (i < N) {
-        float last = 0.0f;
-        float nnt = DONES ? 0.0f : 1.0f - (float)ld[i];     // DONES: set from dones[t] per step
-        float nv = lv[i];
-        GaeChunk<DONES> cur, nxt;
-        gae_load(cur, r, v, es, T - 1, N, i);
-        for (int64_t t0 = T - 1; t0 >= 0; t0 -= GAE_U) {
-            if (t0 - GAE_U >= 0) gae_load(nxt, r, v, es, t0 - GAE_U, N, i);
+    __shared__ float s_r[GAE_TT][64], s_v[GAE_TT][64];
+    __shared__ uint32_t s_e[GAE_TT][16];                 // flags as bytes (4 columns per dword)
+    const int tid = threadIdx.x;
+    const int64_t col0 = (int64_t)blockIdx.x * 64;
+    const int ncol = (int)min<int64_t>(64, N - col0);
+    // this thread's share of a tile: rows ri + 16 * m (m < 4), columns cj .. cj+3
+    const int cj = (tid & 15) * 4, ri = tid >> 4;
+    const bool vec = (N & 3) == 0 && cj + 4 <= ncol;      // 16-B aligned, whole quad in range
+    gf4 pr[4], pv[4], pe[4];
+    auto load_tile = [&](int64_t thi) {                   // rows t = thi - i, i < GAE_TT
 #pragma unroll
-            for (int j = 0; j < GAE_U; j++) {
-                const int64_t t = t0 - j;
-                if (t >= 0) {
-                    const int64_t k = t * N + i;
-                    if (DONES) nnt = 1.0f - cur.e[j];
-                    const float vt = cur.v[j];
-                    const float delta = (cur.r[j] + (g * nv) * nnt) - vt;
-                    last = delta + (c * nnt) * last;
-                    __builtin_nontemporal_store(last, adv + k);
-                    __builtin_nontemporal_store(last + vt, ret + k);
-                    s1 += (double)last;
-                    s2 += (double)last * (double)last;
-                    if (!DONES) nnt = 1.0f - cur.e[j];   // for step t-1: 1 - episode_starts[t]
-                    nv = vt;
+        for (int m = 0; m < 4; m++) {
+            const int64_t t = thi - (ri + 16 * m);
+            pr[m] = pv[m] = pe[m] = gf4{0.f, 0.f, 0.f, 0.f};
+            if (t < 0) continue;
+            const int64_t k = t * N + col0 + cj;
+            if (vec) {
+                pr[m] = __builtin_nontemporal_load(reinterpret_cast<const gf4 *>(r + k));
+                pv[m] = __builtin_nontemporal_load(reinterpret_cast<const gf4 *>(v + k));
+                if (DONES) {
+                    const uint32_t d = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
+                        static_cast<const uint8_t *>(es) + k));
+                    pe[m] = gf4{(float)(d & 0xFF), (float)((d >> 8) & 0xFF), (float)((d >> 16) & 0xFF),
+                                (float)(d >> 24)};
+                } else {
+                    pe[m] = __builtin_nontemporal_load(reinterpret_cast<const gf4 *>(static_cast<const float *>(es) + k));
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (cj + q < ncol) {
+                        pr[m][q] = r[k + q];
+                        pv[m][q] = v[k + q];
+                        pe[m][q] = DONES ? (float)static_cast<const uint8_t *>(es)[k + q]
+                                         : static_cast<const float *>(es)[k + q];
+                    }
                 }
             }
-            cur = nxt;
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const int i = ri + 16 * m;
+            *reinterpret_cast<gf4 *>(&s_r[i][cj]) = pr[m];
+            *reinterpret_cast<gf4 *>(&s_v[i][cj]) = pv[m];
+            s_e[i][cj >> 2] = (uint32_t)pe[m][0] | ((uint32_t)pe[m][1] << 8) | ((uint32_t)pe[m][2] << 16) |
+                              ((uint32_t)pe[m][3] << 24);
+        }
+    };
+    // wave 0 state (lane = column)
+    const int lane = tid & 63;
+    const int64_t col = col0 + lane;
+    const bool active = tid < 64 && lane < ncol;
+    float last = 0.0f, nnt = 0.0f, nv = 0.0f;
+    if (active) {
+        nnt = DONES ? 0.0f : 1.0f - (float)ld[col];
+        nv = lv[col];
+    }
+    double s1 = 0.0, s2 = 0.0;
+    load_tile(T - 1);
+    store_tile();
+    __syncthreads();
+    for (int64_t thi = T - 1; thi >= 0; thi -= GAE_TT) {
+        const bool more = thi - GAE_TT >= 0;
+        if (more) load_tile(thi - GAE_TT);                // next tile in flight during the compute
+        if (active) {
+            const int nrow = (int)min<int64_t>(GAE_TT, thi + 1);
+#pragma unroll 8
+            for (int i = 0; i < nrow; i++) {
+                const int64_t k = (thi - i) * N + col;
+                const float vt = s_v[i][lane], rt = s_r[i][lane];
+                const float et = (float)reinterpret_cast<const uint8_t *>(&s_e[i][0])[lane];
+                if (DONES) nnt = 1.0f - et;
+                const float delta = (rt + (g * nv) * nnt) - vt;
+                last = delta + (c * nnt) * last;
+                __builtin_nontemporal_store(last, adv + k);
+                __builtin_nontemporal_store(last + vt, ret + k);
+                s1 += (double)last;
+                s2 += (double)last * (double)last;
+                if (!DONES) nnt = 1.0f - et;                // for step t-1: 1 - episode_starts[t]
+                nv = vt;
+            }
+        }
+        __syncthreads();                                  // wave 0 is done reading this tile
+        if (more) {
+            store_tile();
+            __syncthreads();
         }
     }
-    if (stats) {
-        __shared__ double red[2][256 / 64];
+    if (stats && tid < 64) {                              // wave 0 holds the sums
         for (int off = 32; off > 0; off >>= 1) {
             s1 += __shfl_down(s1, off);
             s2 += __shfl_down(s2, off);
         }
-        const int w = threadIdx.x >> 6;
-        if ((threadIdx.x & 63) == 0) { red[0][w] = s1; red[1][w] = s2; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double a = 0, b = 0;
-            for (int k = 0; k < (int)(blockDim.x >> 6); k++) { a += red[0][k]; b += red[1][k]; }
-            int64_t cnt = min<int64_t>(blockDim.x, N - (int64_t)blockIdx.x * blockDim.x) * T;
-            atomicAdd(&stats[0], a);
-            atomicAdd(&stats[1], b);
-            atomicAdd(&stats[2], (double)cnt);
+        if (tid == 0) {
+            atomicAdd(&stats[0], s1);
+            atomicAdd(&stats[1], s2);
+            atomicAdd(&stats[2], (double)ncol * (double)T);
         }
     }
 }
@@ -2042,7 +2076,7 @@ mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const floa
     if (!rewards_dev || !values_dev || !episode_starts_dev || !last_values_dev || !last_dones_dev ||
         !advantages_dev || !returns_dev || T <= 0 || N <= 0)
         return fail(MGX_ERR_INVALID, "mgx_gae: bad argument");
-    const int64_t nblk = (N + 255) / 256;
+    const int64_t nblk = (N + 63) / 64;
     hipLaunchKernelGGL(mgx_gae_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, rewards_dev,
                        values_dev, (const void *)episode_starts_dev, last_values_dev, last_dones_dev, T, N, gamma,
                        gamma_lambda, advantages_dev, returns_dev, adv_stats_dev);
@@ -2056,7 +2090,7 @@ mgx_status mgx_gae_dones(const float *rewards_dev, const float *values_dev, cons
     if (!rewards_dev || !values_dev || !dones_dev || !last_values_dev || !advantages_dev || !returns_dev || T <= 0 ||
         N <= 0)
         return fail(MGX_ERR_INVALID, "mgx_gae_dones: bad argument");
-    const int64_t nblk = (N + 255) / 256;
+    const int64_t nblk = (N + 63) / 64;
     hipLaunchKernelGGL(mgx_gae_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, rewards_dev,
                        values_dev, (const void *)dones_dev, last_values_dev, (const uint8_t *)nullptr, T, N, gamma,
                        gamma_lambda, advantages_dev, returns_dev, adv_stats_dev);
