@@ -533,7 +533,7 @@ def measure_rollout(args, layout, world, rank, dev):
                        "gae_launches": nchunks},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
-                         "kernel": "mgx_step_kernel<int, %s>" % ("true> (compact)" if compact else "false> (SB3 stacks)"),
+                         "kernel": ("mgx_step_kernel<int, true> (compact)" if compact else "mgx_step_kernel<int, false> (SB3 stacks)"),
                          "avg_launch_us": per_launch_s * 1e6,
                          "probe_launches": len(probe_us),
                          "step_pipeline_us": float(gpu_ms) * 1e3 / K,

@@ -307,11 +307,15 @@ struct Gen {
         if ((int)__lane_id() == __ffsll((long long)_m) - 1) atomicAdd(&(G).stamps[k], _t - (G).tlast); \
         (G).tlast = _t;                                                                  \
     } while (0)
+#if MGX_GEN_STAMPS == 2          // section clocks only (no per-iteration counters: less distortion)
+#define GCOUNT(G, k) do { } while (0)
+#else
 #define GCOUNT(G, k)                                                                     \
     do {                                                                                 \
         const unsigned long long _m = __ballot(1);                                       \
         if ((int)__lane_id() == __ffsll((long long)_m) - 1) atomicAdd(&(G).stamps[k], 1ull); \
     } while (0)
+#endif
 #else
 #define GSTAMP(G, k) do { } while (0)
 #define GCOUNT(G, k) do { } while (0)
@@ -784,7 +788,9 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
 #pragma unroll 1
     while (!fin) {
         GCOUNT(G, 20);
+        GSTAMP(G, 19);                                           // (commit + task advance of the previous)
         mt_topup(G);
+        GSTAMP(G, 16);                                           // MT window top-up
         int x0, x1, y0, y1;
         room_rect(nr, r, mid, S, x0, x1, y0, y1);
         const bool is_key = phase < 2;
@@ -815,6 +821,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
         const int ex1 = (is_key && !chk) ? -1 : G.ax, ey1 = (is_key && !chk) ? -1 : G.ay;
         const RbConst kx_ = rb_const((uint32_t)(x1 - x0 + 1)), ky_ = rb_const((uint32_t)(y1 - y0 + 1));
         int x, y;
+        GSTAMP(G, 17);                                           // task set-up, choice, satisfiability
         if constexpr (NW <= 2) {
             Bits<NW> bad = G.dn;
             if (!is_key) { bad.w0 |= G.occ.w0; if (NW > 1) bad.w1 |= G.occ.w1; }
@@ -850,6 +857,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
                 }
             }
         }
+        GSTAMP(G, 18);                                           // inner rejection loop
         // commit the placement, then advance to the next task
         const int cidx = cn2idx(cname);
         const int t = is_key ? (kib ? T_BOX : T_KEY) : ot;

@@ -15,7 +15,8 @@ for i in range(64, 256): e.step(acts[i])
 torch.cuda.synchronize()
 c1 = e.debug_counters(); s1 = e.stats()
 names = {8: "copyout+loop", 9: "setup", 10: "mission+nr", 11: "walls+door draws", 12: "door pos",
-         13: "goal+agent", 14: "keys+objects", 15: "mission target"}
+         13: "goal+agent", 14: "keys+objects (last commit)", 15: "mission target", 16: "k+o: MT top-up",
+         17: "k+o: task set-up", 18: "k+o: inner loop", 19: "k+o: commit+advance"}
 waves = (n + 63) // 64; epochs = 192 // e.refill_every
 res = {names[k]: round((c1[k] - c0[k]) / waves / epochs) for k in names}
 res["total_per_wave_epoch"] = sum(res.values())
