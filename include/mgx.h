@@ -203,7 +203,8 @@ mgx_status mgx_get_config(const mgx_handle *h, mgx_config *out);
 /* GAE over a [T][N] f32 rollout (DictRolloutBuffer.compute_returns_and_advantage):
  * episode_starts_dev f32 [T][N], last_values f32 [N], last_dones u8 [N];
  * writes advantages/returns f32 [T][N].  adv_stats_dev (optional, f64 [3]):
- * accumulates (sum A, sum A^2, count) for RCCL advantage-stat reduction. */
+ * accumulates (sum A, sum A^2, count) for RCCL advantage-stat reduction (through a per-device
+ * shard buffer: calls that pass adv_stats_dev must not run concurrently on two streams). */
 mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const float *episode_starts_dev,
                    const float *last_values_dev, const uint8_t *last_dones_dev, int64_t T, int64_t N,
                    float gamma, float gamma_lambda, float *advantages_dev, float *returns_dev,

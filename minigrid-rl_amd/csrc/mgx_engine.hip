@@ -1190,6 +1190,8 @@ __global__ __launch_bounds__(64, 3) void mgx_refill_kernel<1, false>(KParams p) 
 // = 1 - episode_starts[t+1], 1 - last_dones at T-1).
 constexpr int GAE_TT = 64;                 // steps per tile
 typedef float gf4 __attribute__((ext_vector_type(4)));
+constexpr int GAE_SHARDS = 256;
+__device__ double g_gae_shard[GAE_SHARDS][2];   // (sum A, sum A^2) partials; zero between calls
 
 template <bool DONES>
 __global__ __launch_bounds__(256, 4) void mgx_gae_kernel(const float *__restrict__ r, const float *__restrict__ v,
@@ -1292,11 +1294,33 @@ __global__ __launch_bounds__(256, 4) void mgx_gae_kernel(const float *__restrict
             s1 += __shfl_down(s1, off);
             s2 += __shfl_down(s2, off);
         }
-        if (tid == 0) {
-            atomicAdd(&stats[0], s1);
-            atomicAdd(&stats[1], s2);
-            atomicAdd(&stats[2], (double)ncol * (double)T);
+        if (tid == 0) {                                   // sharded: 1024 workgroups on 3 addresses would
+            double *sh = g_gae_shard[blockIdx.x & (GAE_SHARDS - 1)];   // serialise at L2 (~40 us)
+            atomicAdd(&sh[0], s1);
+            atomicAdd(&sh[1], s2);
         }
+    }
+}
+
+// Folds the shards into stats (sum A, sum A^2, count += T*N) and re-zeroes them; runs right after
+// mgx_gae_kernel on the same stream (GAE calls that accumulate stats are stream-ordered).
+__global__ __launch_bounds__(GAE_SHARDS) void mgx_gae_reduce_kernel(double *__restrict__ stats, double count) {
+    __shared__ double red[2][GAE_SHARDS / 64];
+    const int tid = threadIdx.x;
+    double a = g_gae_shard[tid][0], b = g_gae_shard[tid][1];
+    g_gae_shard[tid][0] = 0.0;
+    g_gae_shard[tid][1] = 0.0;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_down(a, off);
+        b += __shfl_down(b, off);
+    }
+    if ((tid & 63) == 0) { red[0][tid >> 6] = a; red[1][tid >> 6] = b; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int k = 1; k < GAE_SHARDS / 64; k++) { a += red[0][k]; b += red[1][k]; }
+        atomicAdd(&stats[0], a);
+        atomicAdd(&stats[1], b);
+        atomicAdd(&stats[2], count);
     }
 }
 
@@ -2081,6 +2105,11 @@ mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const floa
                        values_dev, (const void *)episode_starts_dev, last_values_dev, last_dones_dev, T, N, gamma,
                        gamma_lambda, advantages_dev, returns_dev, adv_stats_dev);
     HIP_TRY(hipGetLastError());
+    if (adv_stats_dev) {
+        hipLaunchKernelGGL(mgx_gae_reduce_kernel, dim3(1), dim3(GAE_SHARDS), 0, (hipStream_t)stream, adv_stats_dev,
+                           (double)T * (double)N);
+        HIP_TRY(hipGetLastError());
+    }
     return MGX_OK;
 }
 
@@ -2095,6 +2124,11 @@ mgx_status mgx_gae_dones(const float *rewards_dev, const float *values_dev, cons
                        values_dev, (const void *)dones_dev, last_values_dev, (const uint8_t *)nullptr, T, N, gamma,
                        gamma_lambda, advantages_dev, returns_dev, adv_stats_dev);
     HIP_TRY(hipGetLastError());
+    if (adv_stats_dev) {
+        hipLaunchKernelGGL(mgx_gae_reduce_kernel, dim3(1), dim3(GAE_SHARDS), 0, (hipStream_t)stream, adv_stats_dev,
+                           (double)T * (double)N);
+        HIP_TRY(hipGetLastError());
+    }
     return MGX_OK;
 }
 
