@@ -14,5 +14,5 @@ cd /tmp && export TMPDIR=/tmp
 P="timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv"
 $P --pmc FETCH_SIZE -d $O/pmcFc -o run -- python3 $R/bench.py --layout compact --steps 256 --warmup 64 --cpu-seconds 0 --probe 0 --graph 0 > $O/pmcFc.log 2>&1 || { tail -20 $O/pmcFc.log; exit 1; }
 $P --pmc WRITE_SIZE -d $O/pmcWc -o run -- python3 $R/bench.py --layout compact --steps 256 --warmup 64 --cpu-seconds 0 --probe 0 --graph 0 > $O/pmcWc.log 2>&1 || { tail -20 $O/pmcWc.log; exit 1; }
-python3 $R/tools/_pmc_summarize.py $O/pmcFc/run_counter_collection.csv $O/pmcWc/run_counter_collection.csv "mgx_step_kernel<int, true>" > $O/pmc_step_kernel_compact.json
+python3 $R/tools/pmc_summarize.py $O/pmcFc/run_counter_collection.csv $O/pmcWc/run_counter_collection.csv "mgx_step_kernel<int, true>" > $O/pmc_step_kernel_compact.json
 cat $O/pmc_step_kernel_compact.json

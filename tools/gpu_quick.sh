@@ -6,7 +6,7 @@ O=$R/gpurun_out
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_vec_env.py -x -q --timeout 300 --timeout-method thread -rf > $O/gpu_tests.log 2>&1 || { tail -60 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
-MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_gstamps.so timeout -k 10 200 python tools/_diag_gen.py > $O/diag_gen.json 2>$O/diag_gen.err || { tail -20 $O/diag_gen.err; exit 1; }
+MGX_LIB_PATH=$R/minigrid-rl_amd/mgx/libmgx_gstamps.so timeout -k 10 200 python tools/diag_gen.py > $O/diag_gen.json 2>$O/diag_gen.err || { tail -20 $O/diag_gen.err; exit 1; }
 cat $O/diag_gen.json
 timeout -k 10 300 python bench.py --steps 1024 --cpu-seconds 0 > $O/bench1k.json 2>$O/bench1k.err || { tail -20 $O/bench1k.err; exit 1; }
 python3 -c "

@@ -26,6 +26,6 @@ for L in compact sb3; do
   $P --pmc FETCH_SIZE -d $O/pmcF_$L -o run -- python3 $R/bench.py --layout $L --steps 256 --warmup 64 --cpu-seconds 0 --probe 0 --graph 0 --both-layouts 0 > $O/pmcF_$L.log 2>&1 || { tail -20 $O/pmcF_$L.log; exit 1; }
   $P --pmc WRITE_SIZE -d $O/pmcW_$L -o run -- python3 $R/bench.py --layout $L --steps 256 --warmup 64 --cpu-seconds 0 --probe 0 --graph 0 --both-layouts 0 > $O/pmcW_$L.log 2>&1 || { tail -20 $O/pmcW_$L.log; exit 1; }
 done
-python3 $R/tools/_pmc_summarize.py $O/pmcF_compact/run_counter_collection.csv $O/pmcW_compact/run_counter_collection.csv "mgx_step_kernel<int, true>" > $O/pmc_step_kernel_compact.json
-python3 $R/tools/_pmc_summarize.py $O/pmcF_sb3/run_counter_collection.csv $O/pmcW_sb3/run_counter_collection.csv "mgx_step_kernel<int, false>" > $O/pmc_step_kernel.json
+python3 $R/tools/pmc_summarize.py $O/pmcF_compact/run_counter_collection.csv $O/pmcW_compact/run_counter_collection.csv "mgx_step_kernel<int, true>" > $O/pmc_step_kernel_compact.json
+python3 $R/tools/pmc_summarize.py $O/pmcF_sb3/run_counter_collection.csv $O/pmcW_sb3/run_counter_collection.csv "mgx_step_kernel<int, false>" > $O/pmc_step_kernel.json
 cat $O/pmc_step_kernel_compact.json $O/pmc_step_kernel.json
