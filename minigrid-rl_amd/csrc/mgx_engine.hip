@@ -90,7 +90,7 @@ struct KParams {
     int cap;                // episodes an env produces per epoch beyond what the invariant needs (<0: fill to D)
     int initial_fill;       // this refill launch is mgx_reset's (fill every ring to 2K)
     int reset_mode;         // mgx_reset: 0 first (seeded, MT cursor 0), 1 seeded, 2 unseeded
-    int stagger;            // diagnostics (env MGX_STAGGER): odd step workgroups start this many clocks late
+    int step_prio;          // s_setprio of the step kernel's waves (env MGX_STEP_PRIO, 0..3)
 };
 
 struct KOut {
@@ -437,7 +437,11 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // 1..147); staged path: smem = image stacks [64][IMG] (new frame in slot 0 of a row).
     const bool fast = !COMPACT && p.fast_roll;
     uint8_t *s_stk = smem;
-    uint8_t *s_grid = smem + p.stk_step;         // grids, chunk-major [GS/16][64 lanes][16 B] (cm_off)
+    // COMPACT keeps no token staging and only [64][148] frame rows: 20.3 KB at S=8, so four step
+    // workgroups fit beside the refill's four waves in a CU's 160 KB (4 x 20.3 + 4 x 17.4); with
+    // the SB3 layout's 25.8 KB only three did, and the fourth waited for a second round
+    constexpr int CSTK = (BLOCK_ENVS * FROW + 15) & ~15;
+    uint8_t *s_grid = smem + (COMPACT ? CSTK : p.stk_step);   // grids, chunk-major [GS/16][64 lanes][16 B] (cm_off)
     uint8_t *s_pgrid = s_grid + BLOCK_ENVS * p.GS;   // popped episodes' grids, same layout
     // LDS-DMA destinations are lane-linear (kept in the dynamic segment: hipcc 7.2 emitted no
     // M0 setup for a static __shared__ destination)
@@ -445,8 +449,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     uint4 *s_tokA = s_phdr + BLOCK_ENVS;         // per lane: the current mission's tokens 0..15,
     uint4 *s_tokB = s_tokA + BLOCK_ENVS;         // 16..31 (envs whose stack is still filling)
     uint4 *s_ptokA = s_tokB + BLOCK_ENVS;        // ... and the popped episode's mission tokens
-    uint4 *s_ptokB = s_ptokA + BLOCK_ENVS;
-    uint4 *s_prng = s_ptokB + BLOCK_ENVS;        // [2][64] the popped episode's RNG snapshot
+    uint4 *s_ptokB = s_ptokA + BLOCK_ENVS;       // (none of the four in COMPACT)
+    uint4 *s_prng = COMPACT ? s_phdr + BLOCK_ENVS : s_ptokB + BLOCK_ENVS;   // [2][64] popped RNG snapshot
     const int IMG = p.img_bytes;
     const int FSTRIDE = (fast || COMPACT) ? FROW : IMG, FOFF = (fast || COMPACT) ? 1 : 0;
     __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params ax | ay<<8 | dir<<16 | carry<<24
@@ -467,10 +471,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     const int ne = (int)min<int64_t>(BLOCK_ENVS, p.n - e0);
     const int S = p.S;
     if (tid == 0) s_ll = 0;
-    if (p.stagger && (blockIdx.x & 1)) {          // diagnostics: desynchronise the workgroups' phases
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)p.stagger) __builtin_amdgcn_s_sleep(8);
-    }
+    // issue priority over the refill's waves on the same SIMD (MGX_STEP_PRIO; wave-uniform)
+    if (p.step_prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (p.step_prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (p.step_prio == 3) __builtin_amdgcn_s_setprio(3);
 #ifdef MGX_STAMPS
     const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
     unsigned long long ts1 = 0, ts2 = 0, tsA = 0, tsB = 0, tsC = 0;
@@ -570,8 +574,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         if (spec) {
             const int64_t slot = (e0 + tid) * p.D + (rhead & (p.D - 1));
             __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot, s_phdr, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 1, s_ptokA, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 2, s_ptokB, 16, 0, 0);
+            if (!COMPACT) {
+                __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 1, s_ptokA, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 2, s_ptokB, 16, 0, 0);
+            }
             __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot, s_prng, 16, 0, 0);
             __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot + 1, s_prng + BLOCK_ENVS, 16, 0, 0);
             const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
@@ -1568,7 +1574,7 @@ struct mgx_handle {
     mgx_config cfg;
     int device;
     KParams kp;
-    size_t lds_step, lds_reset, lds_refill;
+    size_t lds_step, lds_step_compact, lds_reset, lds_refill;
     int nw;                 // 64-bit words of the generator's S*S cell masks (1, 2 or 4)
     bool ext;               // generator variant with full / drp / mov / obstacles
     int refill_every;       // K: steps per refill epoch
@@ -1678,8 +1684,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     {
         const char *sv = std::getenv("MGX_SERIAL_REFILL");
         h->serial_refill = sv && sv[0] == '1';
-        const char *st = std::getenv("MGX_STAGGER");
-        h->kp.stagger = st ? std::atoi(st) : 0;
+        const char *st = std::getenv("MGX_STEP_PRIO");
+        h->kp.step_prio = st ? std::atoi(st) : 0;
     }
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 24;
     h->cfg.mt_table_words = (h->cfg.mt_table_words + MT_FIELDS - 1) / MT_FIELDS * MT_FIELDS;
@@ -1821,8 +1827,10 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->lds_reset = (size_t)p.stk_lds + (size_t)p.grid_lds;
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
-    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
-    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
+    h->lds_step_compact = (size_t)((BLOCK_ENVS * FROW + 15) & ~15) + (size_t)BLOCK_ENVS * 2 * GS   // frame rows + grids
+                          + (size_t)BLOCK_ENVS * 3 * 16;                                     // + popped header, RNG snapshot
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
     h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
     h->ext = cfg->obstacles || cfg->problem == MGX_PROBLEM_FULL || cfg->problem == MGX_PROBLEM_DRP ||
              cfg->problem == MGX_PROBLEM_MOV;
@@ -2041,10 +2049,10 @@ mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_b
         if (fs != MGX_OK) return fs;
     }
     if (action_bytes == 4)
-        hipLaunchKernelGGL((mgx_step_kernel<int32_t, true>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
+        hipLaunchKernelGGL((mgx_step_kernel<int32_t, true>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step_compact,
                            (hipStream_t)stream, h->kp, o, (const int32_t *)actions_dev);
     else
-        hipLaunchKernelGGL((mgx_step_kernel<int64_t, true>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
+        hipLaunchKernelGGL((mgx_step_kernel<int64_t, true>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step_compact,
                            (hipStream_t)stream, h->kp, o, (const int64_t *)actions_dev);
     HIP_TRY(hipGetLastError());
     h->calls++;
