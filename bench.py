@@ -280,10 +280,11 @@ def main_ppo(args, world, rank, local, dev):
 
 def pick_epoch(K, D=128):
     """Refill epoch E (mgx refill_every) so that the K timed steps are whole epochs: the largest
-    divisor of K in [8, D/2] (a ring must hold 2E episodes); K < 8 -> E = K.  None when K has no
-    such divisor (then E = D/4 and the timed region ends with mgx_join, paying for the whole
-    last epoch's refill)."""
-    for E in range(min(64, D // 2), 7, -1):
+    divisor of K in [8, D/4] (at D/2 the ring invariant 2E <= D makes every epoch refill the rings
+    to full, so each wave runs as many rounds as its busiest lane consumed; at <= D/4 the
+    production cap bounds them); K < 8 -> E = K.  None when K has no such divisor (then E = D/4
+    and the timed region ends with mgx_join, paying for the whole last epoch's refill)."""
+    for E in range(min(32, D // 4), 7, -1):
         if K % E == 0:
             return E
     return K if K < 8 else None

@@ -273,15 +273,15 @@ __device__ __forceinline__ void load_rng(Gen<NW> &G, const KParams &p, int64_t e
     G.pcg.ih = ((uint64_t)i.x << 32) | i.y;
     G.pcg.il = ((uint64_t)i.z << 32) | i.w;
     G.pcg.uinteger = a.x;
-    G.pcg.has = a.y;
+    G.pcg.has = a.y & 1u;           // bits 1..: abandoned attempts not yet reported (mgx_refill_kernel)
     G.cur = (uint64_t)a.z | ((uint64_t)a.w << 32);
     G.gbase = ~0ull >> 1;   // empty window
 }
 template <int NW>
-__device__ __forceinline__ void store_rng(const Gen<NW> &G, const KParams &p, int64_t e) {
+__device__ __forceinline__ void store_rng(const Gen<NW> &G, const KParams &p, int64_t e, uint32_t pending_ll = 0) {
     p.pcg[2 * e] = make_uint4((uint32_t)(G.pcg.sh >> 32), (uint32_t)G.pcg.sh, (uint32_t)(G.pcg.sl >> 32), (uint32_t)G.pcg.sl);
     p.pcg[2 * e + 1] = make_uint4((uint32_t)(G.pcg.ih >> 32), (uint32_t)G.pcg.ih, (uint32_t)(G.pcg.il >> 32), (uint32_t)G.pcg.il);
-    p.aux[e] = make_uint4(G.pcg.uinteger, G.pcg.has, (uint32_t)G.cur, (uint32_t)(G.cur >> 32));
+    p.aux[e] = make_uint4(G.pcg.uinteger, G.pcg.has | (pending_ll << 1), (uint32_t)G.cur, (uint32_t)(G.cur >> 32));
 }
 
 template <int NW>
@@ -1118,14 +1118,17 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         const int space = p.D - level, need = 2 * p.K - level;
         int nfree = p.initial_fill ? need : max(need, p.cap < 0 ? space : min(p.cap, space));
         nfree = min(nfree, space);
+        int nmin = max(need, 0);                   // what the ring invariant requires this epoch
         if (nfree > 0) {
             Gen<NW> G;
             load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
             load_rng(G, p, e);
-            int livelocks = 0;
-            // One attempt per iteration for every lane: a lane whose attempt live-locked
-            // retries while the others already generate their next episode (no wave-wide
-            // wait for the retry), exactly reset_env's retry semantics per env.
+            int livelocks = (int)(p.aux[e].y >> 1);   // abandoned attempts carried over from the last epoch
+            // One attempt per iteration for every lane: a lane whose attempt live-locked retries
+            // while the others already generate their next episode, exactly reset_env's retry
+            // semantics per env.  `nfree` budgets ATTEMPTS: an abandoned attempt costs the lane one
+            // episode of this epoch's production (unless the invariant needs it), not the wave an
+            // extra round -- the retry then continues in the next epoch, its count carried in aux.
             while (nfree > 0) {
                 ResetOut R;
                 G.astart = G.cur;
@@ -1133,11 +1136,15 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
                 mt_sync(G);
                 gen_attempt<NW, EXT>(G, R);
                 if (G.nobjs > p.obj_cap) G.err |= 8u;
-                if (G.abort && ++livelocks <= 100000) continue;
+                if (G.abort && ++livelocks <= 100000) {
+                    if (nfree > nmin) nfree--;
+                    continue;
+                }
                 if (G.abort) G.err |= 4u;           // give up on this env (reported, never silent)
                 R.livelocks = livelocks;
                 livelocks = 0;
                 nfree--;
+                nmin--;
                 const int64_t slot = e * p.D + (tail & (p.D - 1));
                 uint4 *dst = reinterpret_cast<uint4 *>(p.ring_grid + slot * p.GS);
                 for (int c = 0; c < (p.GS >> 4); c++) {
@@ -1151,7 +1158,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
                 if (EXT && p.has_move) p.ring_range[slot] = R.range;
                 tail++;
             }
-            store_rng(G, p, e);
+            store_rng(G, p, e, (uint32_t)livelocks);
             p.ring_tail[e] = tail;                 // published to the step kernel at the next join
             maxcur = G.cur;
             err = G.err;

@@ -13,8 +13,9 @@ nobj = int(os.environ.get("NOBJ", 4))
 mission = os.environ.get("MISSION", "5")
 mission = None if mission == "None" else int(mission)
 n = 65536
-e = MgxEngine(problem="multi", mission=mission, size=int(os.environ.get("S", 8)), num_objects=nobj, n_envs=n,
-              terminal_mode="none", refill_every=32)
+e = MgxEngine(problem=os.environ.get("PROBLEM", "multi"), mission=mission, size=int(os.environ.get("S", 8)),
+              num_objects=nobj, n_envs=n, terminal_mode="none", refill_every=32,
+              all_doors_open=os.environ.get("ADO", "0") == "1")
 acts = torch.randint(0, 7, (1024, n), device="cuda", dtype=torch.int32)
 e.reset()
 for i in range(1024):
