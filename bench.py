@@ -397,8 +397,9 @@ def measure_rollout(args, layout, world, rank, dev):
         else:
             for j in range(H):
                 eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
-        if not aligned and c == K // H - 1:
-            eng.join()                                   # last epoch still forked: pay for all of it
+        if not aligned:
+            eng.join()                                   # an epoch may still be forked: the chunk's graph
+                                                         # must be self-contained, and the region pays for it
         gae_dones(rew, vals, dones, last_v, gamma, lam, stats=st, out=(adv, ret))
 
     nchunks = K // H
