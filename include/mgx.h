@@ -218,6 +218,18 @@ mgx_status mgx_gae_dones(const float *rewards_dev, const float *values_dev, cons
                          const float *last_values_dev, int64_t T, int64_t N, float gamma, float gamma_lambda,
                          float *advantages_dev, float *returns_dev, double *adv_stats_dev, void *stream);
 
+/* Scene record of env `env`'s current episode, for PlaygroundEnv.llm_description /
+ * LLMDescriptionWrapper (environment.py:152-195; manual mode, one env): the episode is
+ * regenerated on the device from the RNG state its generation started from, which only the
+ * inline reset mode keeps (ring_depth = -1).  record (HOST, MGX_SCENE_WORDS u32):
+ *   [0] number of objs entries, [1] agent x | y<<8 | dir<<16, [2] mission id | tx<<8 | ty<<16 |
+ *   target action<<24, [3] abandoned attempts, [4] error bits, [8 .. 8+32) objs entries in
+ *   placement order (type | COLOR_NAMES index<<4 | x<<8 | y<<16 | 1<<24 for a door's key or key
+ *   box), [40 ..) the generated grid, one cell code byte per cell (y*S + x; S <= 16).
+ * Synchronises `stream`. */
+#define MGX_SCENE_WORDS 104
+mgx_status mgx_scene(mgx_handle *h, int64_t env, uint32_t *record, void *stream);
+
 /* Synchronises `stream`, returns the device error bits (MGX_DEVERR_*) and clears them. */
 mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits);
 

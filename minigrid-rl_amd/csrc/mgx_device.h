@@ -458,10 +458,13 @@ __device__ __forceinline__ bool occupied(const Gen<NW> &G, int b) {
     else return G.occ.test(b);
 }
 
+// objs entry: type | cname<<4 | x<<8 | y<<16 | OBJ_KEYFLAG (a door's key / key box, placed by the
+// key task: tells the scene description's key lines from object lines, mgx_scene)
+constexpr uint32_t OBJ_KEYFLAG = 1u << 24;
 template <int NW>
-__device__ __forceinline__ void add_obj(Gen<NW> &G, int t, int cname, int x, int y) {
+__device__ __forceinline__ void add_obj(Gen<NW> &G, int t, int cname, int x, int y, uint32_t flags = 0) {
     if (G.nobjs >= MAX_OBJS) { G.err |= 8u; return; }
-    G.objs[G.nobjs++] = (uint32_t)t | ((uint32_t)(cname & 15) << 4) | ((uint32_t)x << 8) | ((uint32_t)y << 16);
+    G.objs[G.nobjs++] = (uint32_t)t | ((uint32_t)(cname & 15) << 4) | ((uint32_t)x << 8) | ((uint32_t)y << 16) | flags;
     G.tmask |= 1u << t;
 }
 
@@ -536,8 +539,8 @@ __device__ __forceinline__ void place_key(Gen<NW> &G, int x0, int x1, int y0, in
         }
     }
     const int cidx = cn2idx(cname);
-    if (kib) { put(G, x, y, mk_code(T_BOX, cidx, 1)); add_obj(G, T_BOX, cname, x, y); }
-    else { put(G, x, y, mk_code(T_KEY, cidx, 0)); add_obj(G, T_KEY, cname, x, y); }
+    if (kib) { put(G, x, y, mk_code(T_BOX, cidx, 1)); add_obj(G, T_BOX, cname, x, y, OBJ_KEYFLAG); }
+    else { put(G, x, y, mk_code(T_KEY, cidx, 0)); add_obj(G, T_KEY, cname, x, y, OBJ_KEYFLAG); }
     if (kx) { *kx = x; *ky = y; }
 }
 
@@ -862,7 +865,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
         const int cidx = cn2idx(cname);
         const int t = is_key ? (kib ? T_BOX : T_KEY) : ot;
         put(G, x, y, mk_code(t, cidx, (is_key && kib) ? 1 : 0));
-        add_obj(G, t, cname, x, y);
+        add_obj(G, t, cname, x, y, is_key ? OBJ_KEYFLAG : 0u);
         if (is_key) {
             if (phase == 0) { kx = x; ky = y; }
             phase++;

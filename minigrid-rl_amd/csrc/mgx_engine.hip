@@ -91,6 +91,8 @@ struct KParams {
     int initial_fill;       // this refill launch is mgx_reset's (fill every ring to 2K)
     int reset_mode;         // mgx_reset: 0 first (seeded, MT cursor 0), 1 seeded, 2 unseeded
     int step_prio;          // s_setprio of the step kernel's waves (env MGX_STEP_PRIO, 0..3)
+    uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
+                            //        generation (mgx_scene regenerates it), else null
 };
 
 struct KOut {
@@ -350,6 +352,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
             G.cur = (uint64_t)c1.z | ((uint64_t)c1.w << 32);
         }
         G.gbase = ~0ull >> 1;
+        if (p.start_rng) rng_snapshot(G, p.start_rng + 2 * e);
         ResetOut R;
         reset_env<NW, EXT>(G, R);
         if (G.nobjs > p.obj_cap) G.err |= 8u;   // objs list ran past its per-config capacity
@@ -1043,6 +1046,7 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
         Gen<NW> G;
         load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
         load_rng(G, p, e);
+        if (p.start_rng) rng_snapshot(G, p.start_rng + 2 * e);
         ResetOut R;
         reset_env<NW, EXT>(G, R);
         if (G.nobjs > p.obj_cap) G.err |= 8u;   // objs list ran past its per-config capacity
@@ -1186,6 +1190,40 @@ __global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) { refill_body
 template <>
 __global__ __launch_bounds__(64, 3) void mgx_refill_kernel<1, false>(KParams p) {
     refill_body<1, false>(p);
+}
+
+// ============================================================== scene kernel
+// mgx_scene: regenerates env e's current episode from the RNG state its generation started from
+// (inline mode keeps it, p.start_rng) and records what PlaygroundEnv's llm_description is built
+// from (custom_env.py:122-2034): the objs list in placement order (doors, goal, keys flagged
+// OBJ_KEYFLAG, objects), the agent, the mission and the generated grid (door lock bits).
+// One lane; the generator is deterministic, so the record is exactly the episode in play.
+template <int NW, bool EXT>
+__global__ __launch_bounds__(64) void mgx_scene_kernel(KParams p, int64_t e, uint32_t *__restrict__ rec) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    if (threadIdx.x != 0) return;
+    uint8_t *s_grid = smem;
+    uint8_t *s_scr = smem + ((64 * p.GSL + 15) & ~15);
+    Gen<NW> G;
+    load_gen(G, p, e, s_grid, s_scr, 0);
+    const uint4 c0 = p.start_rng[2 * e], c1 = p.start_rng[2 * e + 1], inc = p.pcg[2 * e + 1];
+    G.pcg.sh = ((uint64_t)c0.x << 32) | c0.y;
+    G.pcg.sl = ((uint64_t)c0.z << 32) | c0.w;
+    G.pcg.ih = ((uint64_t)inc.x << 32) | inc.y;
+    G.pcg.il = ((uint64_t)inc.z << 32) | inc.w;
+    G.pcg.uinteger = c1.x;
+    G.pcg.has = c1.y & 1u;
+    G.cur = (uint64_t)c1.z | ((uint64_t)c1.w << 32);
+    G.gbase = ~0ull >> 1;
+    ResetOut R;
+    reset_env<NW, EXT>(G, R);
+    rec[0] = (uint32_t)G.nobjs;
+    rec[1] = (uint32_t)G.ax | ((uint32_t)G.ay << 8) | ((uint32_t)G.adir << 16);
+    rec[2] = (uint32_t)R.mission_id | ((uint32_t)R.tx << 8) | ((uint32_t)R.ty << 16) | ((uint32_t)R.ta << 24);
+    rec[3] = (uint32_t)R.livelocks;
+    rec[4] = G.err;
+    for (int k = 0; k < MAX_OBJS; k++) rec[8 + k] = k < G.nobjs ? G.objs[k] : 0u;
+    for (int k = 0; k < p.S * p.S; k++) reinterpret_cast<uint8_t *>(rec + 8 + MAX_OBJS)[k] = G.g[k];
 }
 
 // ================================================================ GAE kernel
@@ -1825,6 +1863,14 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         p.ring_range = mv ? p.range_cur + N : p.range_cur;
     }
     p.D = D;
+    p.start_rng = nullptr;
+    if (D == 0) {   // inline mode: keep each episode's generation start state (mgx_scene)
+        hipError_t e = hipMalloc(&h->allocs[15], (size_t)N * 32);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc start rng"));
+        e = hipMemset(h->allocs[15], 0, (size_t)N * 32);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset start rng"));
+        p.start_rng = (uint4 *)h->allocs[15];
+    }
     p.K = h->cfg.refill_every;
     p.cap = h->cfg.refill_cap;
     p.initial_fill = 0;
@@ -1850,6 +1896,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->lds_refill = (size_t)((64 * (GS + 4) + 15) & ~15) + (size_t)64 * scratch_per_env(p.obj_stride);
     MGX_SET_LDS(mgx_refill_kernel, h->lds_refill);
     MGX_SET_LDS(mgx_fixup_kernel, h->lds_refill);
+    MGX_SET_LDS(mgx_scene_kernel, h->lds_refill);
 #undef MGX_SET_LDS
 #undef MGX_SET_LDS1
     {
@@ -2105,6 +2152,24 @@ mgx_status mgx_gather(const mgx_handle *h, const uint8_t *rows_dev, const uint8_
     }
 #undef MGX_GATHER
     HIP_TRY(hipGetLastError());
+    return MGX_OK;
+}
+
+mgx_status mgx_scene(mgx_handle *h, int64_t env, uint32_t *record, void *stream) {
+    if (!h || !record) return fail(MGX_ERR_INVALID, "mgx_scene: null argument");
+    if (env < 0 || env >= h->kp.n) return fail(MGX_ERR_INVALID, "mgx_scene: env out of range");
+    if (!h->kp.start_rng) return fail(MGX_ERR_INVALID, "mgx_scene: needs inline resets (ring_depth = -1)");
+    if (h->kp.S * h->kp.S > 4 * (MGX_SCENE_WORDS - 8 - MAX_OBJS)) return fail(MGX_ERR_INVALID, "mgx_scene: grid too large");
+    uint32_t *dev = nullptr;
+    HIP_TRY(hipMalloc(&dev, MGX_SCENE_WORDS * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(dev, 0, MGX_SCENE_WORDS * sizeof(uint32_t), (hipStream_t)stream));
+    MGX_GEN_LAUNCH(mgx_scene_kernel, dim3(1), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, env, dev);
+    hipError_t le = hipGetLastError();
+    hipError_t ce = le == hipSuccess ? hipMemcpyAsync(record, dev, MGX_SCENE_WORDS * sizeof(uint32_t),
+                                                      hipMemcpyDeviceToHost, (hipStream_t)stream) : le;
+    hipError_t se = ce == hipSuccess ? hipStreamSynchronize((hipStream_t)stream) : ce;
+    (void)hipFree(dev);
+    if (se != hipSuccess) return fail(MGX_ERR_HIP, std::string("mgx_scene: ") + hipGetErrorString(se));
     return MGX_OK;
 }
 

@@ -4,8 +4,9 @@ Host-side mirror of the reference's env/rollout interface (Idokorro/MiniGrid-RL
 src/custom_env.py, src/environment.py, src/ppo.py) over libmgx.so (HIP/gfx950).
 """
 from ._lib import MgxError, mission_text  # noqa: F401
+from .describe import LLMDescriptionWrapper  # noqa: F401
 from .engine import MgxEngine, gae, gae_dones  # noqa: F401
 from .evaluation import EvalCallback, StopTrainingOnRewardThreshold, evaluate_policy  # noqa: F401
 from .vec_env import MgxVecEnv  # noqa: F401
 
-__all__ = ["EvalCallback", "MgxEngine", "MgxError", "MgxVecEnv", "StopTrainingOnRewardThreshold", "evaluate_policy", "gae", "gae_dones", "mission_text"]
+__all__ = ["EvalCallback", "LLMDescriptionWrapper", "MgxEngine", "MgxError", "MgxVecEnv", "StopTrainingOnRewardThreshold", "evaluate_policy", "gae", "gae_dones", "mission_text"]

@@ -24,7 +24,7 @@ DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unk
 # Every entry point include/mgx.h declares (checked by tests/test_abi.py).
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
            "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_gae_dones", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text",
-           "mgx_step_compact", "mgx_observe_compact", "mgx_gather")
+           "mgx_step_compact", "mgx_observe_compact", "mgx_gather", "mgx_scene")
 
 
 class MgxConfig(ctypes.Structure):
@@ -99,6 +99,7 @@ def load():
     L.mgx_step_compact.argtypes = [P, P, I, ctypes.POINTER(MgxCompactOut), P]
     L.mgx_observe_compact.argtypes = [P, P, P, P]
     L.mgx_gather.argtypes = [P, P, P, P, I64, P, I64, P, P, I, P, I, P, P]
+    L.mgx_scene.argtypes = [P, I64, ctypes.POINTER(ctypes.c_uint32), P]
     for name in EXPORTS:
         getattr(L, name).restype = getattr(L, name).restype or I
     if L.mgx_abi_version() != ABI_VERSION:

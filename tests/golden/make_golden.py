@@ -211,10 +211,14 @@ def run_config(name, cfg, n, T, seed_actions=1234):
         d[prefix + "pcg"][idx] = pcg_state(env)
 
     alloc("reset0_livelock", (n,), np.int32)
+    # PlaygroundEnv.llm_description of every reset (LLMDescriptionWrapper, environment.py:152-195):
+    # (t, env, text) in reset order, t = -1 for the first reset
+    descs = []
     for i in range(n):
         obs, nll = vec.reset_env(i, seed=cfg.seed + i)
         rec_reset("reset0_", i, i, obs)
         d["reset0_livelock"][i] = nll
+        descs.append((-1, i, vec.envs[i].unwrapped.llm_description))
     missions = {}
     for t in range(T):
         for i in range(n):
@@ -238,7 +242,11 @@ def run_config(name, cfg, n, T, seed_actions=1234):
                 obs2, nll = vec.reset_env(i)
                 d["livelock"][t, i] = nll
                 rec_reset("r_", (t, i), i, obs2)
+                descs.append((t, i, vec.envs[i].unwrapped.llm_description))
     d["actions"] = acts
+    d["desc_t"] = np.array([x[0] for x in descs], np.int32)
+    d["desc_env"] = np.array([x[1] for x in descs], np.int32)
+    d["desc_text"] = np.array([x[2] for x in descs])
     d["meta"] = np.array([S, n, T, cfg.seed, -1 if cfg.env.mission is None else cfg.env.mission,
                           cfg.env.num_objects], np.int64)
     d["problem"] = np.array(cfg.env.problem)

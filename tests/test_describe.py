@@ -1,0 +1,51 @@
+"""LLMDescriptionWrapper / PlaygroundEnv.llm_description (environment.py:152-195, custom_env.py's
+generators) against the reference: every fixture records the llm_description text of every reset
+the reference made (tests/golden/make_golden.py runs the reference); the engine, driven by the
+same actions in the inline reset mode, must rebuild each of them from its scene record."""
+import numpy as np
+import pytest
+
+import trajcheck as TC
+
+torch = pytest.importorskip("torch")
+
+
+def test_mission_tokens_vocab():
+    from mgx.describe import MSN_LEN, VOCAB, mission_tokens
+    assert VOCAB[:6] == [" ", "\n", "-", ":", ",", "."] and VOCAB[6] == "a" and len(VOCAB) == 32
+    t = mission_tokens("The scene contains:\nMission: go to goal")
+    assert t.shape == (MSN_LEN,) and t.dtype == np.int64
+    assert list(t[:4]) == [VOCAB.index("t"), VOCAB.index("h"), VOCAB.index("e"), 0] and t[40:].sum() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", [p for p in TC.fixtures()], ids=lambda p: p.split("/")[-1][:-4])
+def test_llm_description_matches_reference(path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mgx import MgxEngine
+    from mgx.describe import LLMDescriptionWrapper
+    d = dict(np.load(path))
+    if "desc_text" not in d:
+        pytest.skip("fixture without descriptions")
+    cfg, T = TC.fixture_cfg(d)
+    kw = dict(cfg)
+    n = kw.pop("n_envs")
+    problem = kw["problem"]
+    eng = MgxEngine(n_envs=n, ring_depth=-1, terminal_mode="none", **kw)
+    wrap = LLMDescriptionWrapper(eng, problem)
+    eng.reset()
+    want = {}
+    for t, i, txt in zip(d["desc_t"], d["desc_env"], d["desc_text"]):
+        want.setdefault(int(t), {})[int(i)] = str(txt)
+    T = min(T, 200)
+    for i in range(n):
+        assert wrap.description(i) == want[-1][i], ("first reset", i)
+    checked = n
+    for t in range(T):
+        eng.step(torch.as_tensor(d["actions"][t].astype(np.int32), device=eng.device))
+        for i, txt in want.get(t, {}).items():
+            assert wrap.description(i) == txt, (t, i)
+            checked += 1
+    assert checked > n
+    eng.poll_error()

@@ -5,7 +5,8 @@ import torch
 from mgx import MgxEngine
 n = int(os.environ.get("N", 65536)); mission = os.environ.get("MISSION", "5")
 mission = None if mission == "None" else int(mission)
-e = MgxEngine(problem="multi", mission=mission, size=int(os.environ.get("S", 8)), n_envs=n)
+e = MgxEngine(problem="multi", mission=mission, size=int(os.environ.get("S", 8)), n_envs=n,
+              all_doors_open=os.environ.get("ADO", "0") == "1", num_objects=int(os.environ.get("NOBJ", 4)))
 acts = torch.randint(0, 7, (256, n), device="cuda", dtype=torch.int32)
 e.reset()
 for i in range(64): e.step(acts[i])
