@@ -344,11 +344,11 @@ def measure_rollout(args, layout, world, rank, dev):
                     refill_every=E or 0, refill_cap=args.refill_cap, ring_depth=args.ring_depth)
     E = eng.refill_every
     H = pick_horizon(K, E if aligned else None, args.horizon or 0)
-    # warm-up: whole refill epochs, and at least 640 steps -- the rings start at 2E episodes and
-    # fill towards D (at most `refill_cap` per env per epoch beyond consumption); a shorter
-    # warm-up would time that fill-up (the refill producing ~2x what the steps consume), not the
-    # steady state, where production = consumption (`window` reports both)
-    W = -(-max(args.warmup, 640) // E) * E
+    # warm-up: whole refill epochs, and at least 2,048 steps -- the rings start at 2E episodes and
+    # fill towards D at (cap - consumption) per env per epoch, ~1.3 episodes per 32 steps; a
+    # shorter warm-up would time that fill-up (the refill producing more than the steps consume),
+    # not the steady state, where production = consumption (`window` reports both)
+    W = -(-max(args.warmup, 2048) // E) * E
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     P = args.probe

@@ -84,7 +84,8 @@ typedef struct mgx_config {
     int32_t terminal_mode;     /* mgx_terminal_mode */
     int32_t mission_int64;     /* 1: mission tokens int64 (TokenizeVocabWrapper dtype), 0: uint8 */
     int32_t refill_cap;        /* episodes an env may pre-generate per refill epoch beyond what keeps the
-                                  ring from running dry (0 -> 6, < 0 -> fill the ring) */
+                                  ring from running dry (0 -> max(2, round(0.19 * refill_every)), i.e. 6
+                                  at the default epoch; < 0 -> fill the ring) */
     int64_t mt_table_words;    /* 0 -> default (2^24); shared MT19937 output table length */
     int32_t ring_depth;        /* pre-generated episodes per env (0 -> 128; rounded up to a power of two
                                   <= 128; -1 = no ring: every auto-reset generated inline) */

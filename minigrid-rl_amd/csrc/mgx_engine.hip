@@ -1149,6 +1149,10 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
                 livelocks = 0;
                 nfree--;
                 nmin--;
+                // the mission's tokens first: issued before any store to the ring (which the compiler
+                // must assume may alias the table), their latency overlaps the grid copy-out
+                const uint4 tok0 = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[0];
+                const uint4 tok1 = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[1];
                 const int64_t slot = e * p.D + (tail & (p.D - 1));
                 uint4 *dst = reinterpret_cast<uint4 *>(p.ring_grid + slot * p.GS);
                 for (int c = 0; c < (p.GS >> 4); c++) {
@@ -1156,8 +1160,8 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
                     dst[c] = make_uint4(q[0], q[1], q[2], q[3]);
                 }
                 p.ring_hdr[3 * slot] = pack_hdr(G, R);
-                p.ring_hdr[3 * slot + 1] = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[0];
-                p.ring_hdr[3 * slot + 2] = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[1];
+                p.ring_hdr[3 * slot + 1] = tok0;
+                p.ring_hdr[3 * slot + 2] = tok1;
                 rng_snapshot(G, p.ring_rng + 2 * slot);
                 if (EXT && p.has_move) p.ring_range[slot] = R.range;
                 tail++;
@@ -1722,7 +1726,9 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     }
     if (h->cfg.refill_every <= 0) h->cfg.refill_every = std::max(1, h->cfg.ring_depth / 4);
     if (h->cfg.refill_every > h->cfg.ring_depth / 2) h->cfg.refill_every = std::max(1, h->cfg.ring_depth / 2);
-    if (h->cfg.refill_cap == 0) h->cfg.refill_cap = 6;
+    // default production cap: ~1.3x a random policy's consumption (1 in 7 steps ends an episode on
+    // 'done' alone; 0.146 resets per env-step measured at config 2), i.e. 6 at the default epoch of 32
+    if (h->cfg.refill_cap == 0) h->cfg.refill_cap = std::max(2, (h->cfg.refill_every * 19 + 50) / 100);
     h->refill_every = h->cfg.refill_every;
     h->calls = 0;
     h->in_flight = false;
