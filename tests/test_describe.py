@@ -49,3 +49,28 @@ def test_llm_description_matches_reference(path):
             checked += 1
     assert checked > n
     eng.poll_error()
+
+
+def test_llm_description_formatting_from_a_record():
+    """The formatter on a hand-made 2-room scene record: the layout and door lines, then per room
+    robot / door keys / goal / objects in placement order (custom_env.py:617-725)."""
+    from mgx.describe import KEYFLAG, llm_description
+    S = 8
+    grid = np.full((S, S), 1, np.uint8)
+    grid[3, 4] = 4 | (4 << 4) | 0x80                                   # locked door at x=4, y=3
+    objs = [dict(type=4, color=5, x=4, y=3, key=False),                # yellow door
+            dict(type=8, color=15, x=6, y=2, key=False),               # goal, right room
+            dict(type=7, color=5, x=2, y=5, key=True),                 # key box for the door, left room
+            dict(type=6, color=0, x=1, y=1, key=False),                # blue ball, left
+            dict(type=5, color=3, x=5, y=6, key=False)]                # purple key, right
+    sc = dict(objs=objs, agent=(2, 2, 0), mission_id=3, grid=grid, size=S)
+    assert llm_description(sc, "multi") == (
+        "The scene contains:\nTwo rooms. Left and right.\n"
+        "There is a locked yellow door between the rooms\n"
+        "Left room contains:\n- robot\n- yellow box\n- blue ball\n"
+        "Right room contains:\n- goal\n- purple key\nMission: ")
+    assert KEYFLAG == 1 << 24
+    single = dict(objs=[dict(type=6, color=1, x=1, y=1, key=False), dict(type=8, color=15, x=2, y=2, key=False)],
+                  agent=(3, 3, 0), mission_id=3, grid=grid, size=S)
+    assert llm_description(single, "gtg").endswith("- green ball\n- goal\nMission: ")
+    assert llm_description(single, "drp").endswith("- green ball\nMission: ")     # the drop map's quirk
