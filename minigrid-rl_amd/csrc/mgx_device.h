@@ -754,11 +754,13 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     // of the 3/4-room layouts loops over the upper-left counter).  No RNG involved.
     uint32_t keymask = 0;   // room r: bit 2r = key A placed, bit 2r+1 = key B placed
     uint32_t npack = 0;     // room r: byte r = objects to place (clamped at 0)
+    uint32_t kspec = 0;     // room r: bits 4r..4r+3 = door of key A, key B (2 bits each); bit 16+r = chk
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         int kA, kB;
         bool chk;
         key_spec(nr, r, ar, kA, kB, chk);
+        kspec |= (uint32_t)(kA & 3) << (4 * r) | (uint32_t)(kB & 3) << (4 * r + 2) | (uint32_t)chk << (16 + r);
         const bool a = r < nr && kA >= 0 && ((dinfo >> (8 * kA + 3)) & 1);
         const bool b = r < nr && kB >= 0 && ((dinfo >> (8 * kB + 3)) & 1);
         keymask |= (uint32_t)a << (2 * r) | (uint32_t)b << (2 * r + 1);
@@ -800,9 +802,8 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
         int cname, ot = T_KEY, ox = -1, oy = -1;
         bool chk = false, kib = false;
         if (is_key) {
-            int kA, kB;
-            key_spec(nr, r, ar, kA, kB, chk);
-            const uint32_t di = dinfo >> (8 * (phase == 0 ? kA : kB));
+            chk = (kspec >> (16 + r)) & 1;
+            const uint32_t di = dinfo >> (8 * ((kspec >> (4 * r + 2 * phase)) & 3));
             cname = di & 7;
             kib = (di >> 4) & 1;
             if (phase == 1) { ox = kx; oy = ky; }

@@ -4,7 +4,7 @@ set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out
 mkdir -p $O
-for EC in "32 5" "32 6" "16 3" "16 4" "24 4" "24 5"; do
+for EC in "32 5" "32 6" "32 7" "32 5" "32 6"; do
   set -- $EC; E=$1; C=$2
   timeout -k 10 120 python bench.py --steps 2048 --warmup 2048 --cpu-seconds 0 --both-layouts 0 --refill-every $E --refill-cap $C > $O/sw.json 2>$O/sw.err || { tail -5 $O/sw.err; exit 1; }
   python3 -c "
