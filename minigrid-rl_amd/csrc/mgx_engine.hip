@@ -391,35 +391,47 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
 // layout: one 16-B chunk per lane per global_load_lds); byte b of lane le's grid:
 __device__ __forceinline__ int cm_off(int le, int b) { return (b >> 4) * (BLOCK_ENVS * 16) + le * 16 + (b & 15); }
 
-// Render cells [13q, 13q + 13) of env slot `le`'s 7x7 view (c = vx*7 + vy; q = 3 holds the
-// last 10) into a frame row fr ([type 49][colour 49][state 49]).  The view is closed form:
-// cell (vx, vy) = A + (6 - vy) * dir_vec + (vx - 3) * right_vec (minigrid's slice + (dir+1)
-// rotate_left), out of bounds -> Wall, (3, 6) -> carried object or None.  `grids` is the
-// block's current grids or its popped episodes' grids (both chunk-major).
-// All thirteen grid bytes are read before any frame byte is written: one LDS round trip.
-__device__ __forceinline__ void render13(const uint8_t *grids, int S, int le, int q, uint32_t rp, uint8_t *fr) {
+// Render the view columns thread q (0..3) of env slot `le` owns -- vx = q and q + 4; thread 3
+// only column 3, which holds the agent's own cell (3, 6) -- into a frame row fr ([type 49]
+// [colour 49][state 49], cell c = vx*7 + vy).  The view is closed form: cell (vx, vy) = A +
+// (6 - vy) * dir_vec + (vx - 3) * right_vec (minigrid's slice + (dir+1) rotate_left); (3, 6)
+// -> carried object or None.  Out-of-grid cells are Wall, and so is every border cell of a
+// grid (custom_env.py:132 wall_rect; no action can replace a wall), so a coordinate clamped
+// as unsigned to S-1 (negative -> S-1, the far border) reads a Wall exactly when it is out of
+// the grid: no bounds test, no select.
+// Along a column the world cell moves by -dir_vec per vy (adds only, no multiplies).  `grids`
+// is the block's current grids or its popped episodes' grids (both chunk-major).  Every grid
+// byte is read before any frame byte is written: one LDS round trip.
+__device__ __forceinline__ void render_cols(const uint8_t *grids, int S, int le, int q, uint32_t rp, uint8_t *fr) {
     const int ax = rp & 0xFF, ay = (rp >> 8) & 0xFF, dir = (rp >> 16) & 3;
     const uint8_t carry = (uint8_t)(rp >> 24);
     const int dx = (dir == 0) - (dir == 2), dy = (dir == 1) - (dir == 3);
-    uint8_t code[13];
+    const uint8_t *base = grids + le * 16;
+    uint8_t code[2][7];
 #pragma unroll
-    for (int k = 0; k < 13; k++) {
-        const int c = 13 * q + k;
-        const int vx = (c * 37) >> 8, vy = c - vx * 7;                 // c / 7 for c < 52
-        const int wx = ax + (6 - vy) * dx - (vx - 3) * dy;              // right_vec = (-dy, dx)
-        const int wy = ay + (6 - vy) * dy + (vx - 3) * dx;
-        const bool in = (unsigned)wx < (unsigned)S && (unsigned)wy < (unsigned)S;
-        const uint8_t g = grids[cm_off(le, in ? wy * S + wx : 0)];
-        code[k] = c == 3 * 7 + 6 ? (carry ? carry : CODE_EMPTY) : (in ? g : CODE_WALL);
+    for (int j = 0; j < 2; j++) {
+        const int ox = q + 4 * j - 3;                                   // vx - 3 (column 7: unused)
+        int wx = ax + 6 * dx - __mul24(ox, dy), wy = ay + 6 * dy + __mul24(ox, dx);
+#pragma unroll
+        for (int vy = 0; vy < 7; vy++) {
+            const uint32_t cx = min((uint32_t)wx, (uint32_t)(S - 1)), cy = min((uint32_t)wy, (uint32_t)(S - 1));
+            const int b = (int)__umul24(cy, (uint32_t)S) + (int)cx;
+            code[j][vy] = base[b + __mul24(b >> 4, BLOCK_ENVS * 16 - 16)];   // cm_off(le, b)
+            wx -= dx;
+            wy -= dy;
+        }
     }
+    if (q == 3) code[0][6] = carry ? carry : CODE_EMPTY;
 #pragma unroll
-    for (int k = 0; k < 13; k++) {
-        const int c = 13 * q + k;
-        if (c < 49) {
-            const uint32_t v = encode3(code[k]);
-            fr[c] = (uint8_t)v;
-            fr[49 + c] = (uint8_t)(v >> 8);
-            fr[98 + c] = (uint8_t)(v >> 16);
+    for (int j = 0; j < 2; j++) {
+        if (j == 1 && q == 3) break;
+        const int c0 = 7 * (q + 4 * j);
+#pragma unroll
+        for (int vy = 0; vy < 7; vy++) {
+            const uint32_t v = code[j][vy], t = v & 15u;
+            fr[c0 + vy] = (uint8_t)(t == T_OPEN ? (uint32_t)T_DOOR : t);
+            fr[49 + c0 + vy] = (uint8_t)__builtin_amdgcn_ubfe(v, 4, 3);
+            fr[98 + c0 + vy] = (uint8_t)(t == T_DOOR ? 1u + (v >> 7) : 0u);
         }
     }
 }
@@ -809,7 +821,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     if (s_tmask) {
         {
             const int le = tid >> 2, q = tid & 3;
-            if (le < ne && s_term[le]) render13(s_grid, S, le, q, s_rp[le], s_stk + le * FSTRIDE + FOFF);
+            if (le < ne && s_term[le]) render_cols(s_grid, S, le, q, s_rp[le], s_stk + le * FSTRIDE + FOFF);
         }
         __syncthreads();
         if (p.vis) {
@@ -845,7 +857,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         if (le < ne) {
             const bool pop = s_popf[le];
             const uint32_t rp = pop ? s_rp2[le] : s_rp[le];
-            render13(pop ? s_pgrid : s_grid, S, le, q, rp, s_stk + le * FSTRIDE + FOFF);
+            render_cols(pop ? s_pgrid : s_grid, S, le, q, rp, s_stk + le * FSTRIDE + FOFF);
             if (COMPACT && q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);   // row byte 0: direction
         }
     }
