@@ -633,71 +633,62 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         const bool done_e = (a == A_FORWARD && (ft == T_GOAL || ft == T_LAVA)) || a == A_DONE || sc >= ms;
         const bool avail = done_e && spec;
         const bool filling = !COMPACT && !done_e && st.frames < p.n_stack;
-        double rew = 0.0;
-        switch (a) {                                   // MiniGridEnv.step (3P)
-            case A_LEFT: dir = (dir + 3) & 3; break;
-            case A_RIGHT: dir = (dir + 1) & 3; break;
-            case A_FORWARD:
-                if (can_overlap(fc)) { ax = fx; ay = fy; }
-                if (ft == T_GOAL) { term = true; rew = reward_at(sc, ms); }
-                if (ft == T_LAVA) term = true;
-                break;
-            case A_PICKUP:
-                if (can_pickup(fc) && carry == 0) { carry = fc; *fp = CODE_EMPTY; dirty = true; }
-                break;
-            case A_DROP:
-                if (ft == T_EMPTY && carry != 0) { *fp = carry; carry = 0; dirty = true; }
-                break;
-            case A_TOGGLE:
-                if (ft == T_DOOR) {
-                    if (fc >> 7) {                     // locked: needs a Key of the door's colour
-                        if ((carry & 15) == T_KEY && ((carry >> 4) & 7) == ((fc >> 4) & 7)) {
-                            *fp = mk_code(T_OPEN, (fc >> 4) & 7, 0); dirty = true;
-                        }
-                    } else { *fp = mk_code(T_OPEN, (fc >> 4) & 7, 0); dirty = true; }
-                } else if (ft == T_OPEN) {
-                    *fp = mk_code(T_DOOR, (fc >> 4) & 7, 0); dirty = true;
-                } else if (ft == T_BOX) {
-                    *fp = (fc >> 7) ? mk_code(T_KEY, (fc >> 4) & 7, 0) : CODE_EMPTY; dirty = true;
-                }
-                break;
-            default: break;                            // done (and invalid) -> no-op
-        }
+        // MiniGridEnv.step (3P), as selects: every action's outcome is computed and the taken
+        // one kept (a branch per action made a divergent tree of exec-mask updates -- half of
+        // this phase's instructions were SALU mask bookkeeping)
+        const bool isF = a == A_FORWARD, isT = a == A_TOGGLE;
+        const int fcol = (fc >> 4) & 7;
+        dir = (dir + (a == A_RIGHT) + 3 * (a == A_LEFT)) & 3;
+        const bool mv = isF && can_overlap(fc);
+        ax = mv ? fx : ax;
+        ay = mv ? fy : ay;
+        const bool goal = isF && ft == T_GOAL;
+        term = goal || (isF && ft == T_LAVA);
+        const bool pick = a == A_PICKUP && can_pickup(fc) && carry == 0;
+        const bool drop = a == A_DROP && ft == T_EMPTY && carry != 0;
+        // toggle: a locked door opens only with a Key of its colour; an open door closes; a
+        // box turns into its contents (the key it holds, or nothing)
+        const bool t_door = isT && ft == T_DOOR &&
+                            (!(fc >> 7) || ((carry & 15) == T_KEY && ((carry >> 4) & 7) == fcol));
+        const bool t_open = isT && ft == T_OPEN, t_box = isT && ft == T_BOX;
+        uint8_t nc = fc;
+        nc = t_door ? mk_code(T_OPEN, fcol, 0) : nc;
+        nc = t_open ? mk_code(T_DOOR, fcol, 0) : nc;
+        nc = t_box ? ((fc >> 7) ? mk_code(T_KEY, fcol, 0) : CODE_EMPTY) : nc;
+        nc = pick ? CODE_EMPTY : nc;
+        nc = drop ? carry : nc;
+        carry = pick ? fc : (drop ? (uint8_t)0 : carry);
+        dirty = pick || drop || t_door || t_open || t_box;
+        if (dirty) *fp = nc;
         trunc = sc >= ms;
         // gen_obs() is taken here, before PlaygroundEnv's key consumption (Q3)
         s_rp[tid] = (uint32_t)ax | ((uint32_t)ay << 8) | ((uint32_t)dir << 16) | ((uint32_t)carry << 24);
-        // ---- PlaygroundEnv.step (custom_env.py:269-330)
-        mdone = st.mission_done;
-        rs = st.reward_step;
+        // ---- PlaygroundEnv.step (custom_env.py:269-330), as selects
+        const int md0 = st.mission_done, rs0 = st.reward_step;
         const bool is_gtg = st.mission_id == CMD_GOTOGOAL;
-        if (term) {
-            if (!is_gtg) { mdone = 0; rs = -1; rew = 0.0; }
-        } else {
-            if (a == A_TOGGLE) {
-                const uint8_t f2 = *fp;
-                if (is_door(f2) && carry != 0 && ((f2 >> 4) & 7) == ((carry >> 4) & 7)) carry = 0;  // Q4
-            }
-            if (!mdone) {
-                const bool has_t = st.tx != NONE8;
-                bool arrived = false;
-                if (has_t) {
-                    if (st.target_action != NONE8 && st.target_action != 0) {
-                        const int nfx = ax + ((dir == 0) - (dir == 2)), nfy = ay + ((dir == 1) - (dir == 3));
-                        arrived = nfx == st.tx && nfy == st.ty;
-                    } else if (ax == st.tx && ay == st.ty) {
-                        if (rs < 0) rs = sc;
-                        mdone = 1;
-                    }
-                }
-                if (arrived && a == (int)st.target_action) { if (rs < 0) rs = sc; mdone = 1; }
-                if (!has_t && st.target_action != NONE8 && a == (int)st.target_action) { if (rs < 0) rs = sc; mdone = 1; }
-                if (st.mission_id >= MID_MOVE && in_move_range(mrange, ax, ay)) { if (rs < 0) rs = sc; mdone = 1; }
-            }
-            if (a == A_DONE) {
-                rew = mdone ? reward_at(rs, ms) : 0.0;    // stored self.reward, or 0 (not manual)
-                mdone = 0; rs = -1; term = true;
-            }
-        }
+        const bool t0 = term;
+        // Q4: toggling a door while carrying a key of its colour consumes the key (not on a
+        // terminating step)
+        if (!t0 && isT && is_door(nc) && carry != 0 && ((nc >> 4) & 7) == ((carry >> 4) & 7)) carry = 0;
+        // mission completed this step (each test only sets `reward_step` if unset, `done` flag)
+        const int ta = st.target_action;
+        const bool has_t = st.tx != NONE8, ta_fwd = ta != NONE8 && ta != 0;
+        const int nfx = ax + ((dir == 0) - (dir == 2)), nfy = ay + ((dir == 1) - (dir == 3));
+        // (bitwise & / |: short-circuit operators turned this into a nest of branches)
+        const bool at_f = (nfx == st.tx) & (nfy == st.ty), at_a = (ax == st.tx) & (ay == st.ty);
+        const bool hit = (!t0 & !md0) &
+                         ((has_t & ta_fwd & at_f & (a == ta)) | (has_t & !ta_fwd & at_a) |
+                          (!has_t & (ta != NONE8) & (a == ta)) |
+                          ((st.mission_id >= MID_MOVE) & in_move_range(mrange, ax, ay)));
+        const int md1 = hit ? 1 : md0, rs1 = (hit && rs0 < 0) ? sc : rs0;
+        const bool dn = !t0 && a == A_DONE;         // 'done': the stored self.reward, or 0 (not manual)
+        // reward: reaching the goal pays 1 - 0.9 sc/ms only on 'go to goal' missions; 'done'
+        // pays the reward stored at mission completion
+        double rew = 0.0;
+        if ((goal && is_gtg) || (dn && md1)) rew = reward_at(t0 ? sc : rs1, ms);
+        mdone = t0 ? (is_gtg ? md0 : 0) : (dn ? 0 : md1);
+        rs = t0 ? (is_gtg ? rs0 : -1) : (dn ? -1 : rs1);
+        term = t0 || dn;
         done = term || trunc;
         const bool tw = done && (p.terminal_mode == MGX_TERMINAL_ALL ||
                                  (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term));
