@@ -1086,7 +1086,9 @@ template <int NW>
 __device__ __forceinline__ void gen_init(Gen<NW> &G) {}
 
 // One attempt of MiniGridEnv.reset -> PlaygroundEnv._gen_grid (custom_env.py:122-267).
-template <int NW, bool EXT>
+// MULTI: the problem is known to be 'multi' (every BASELINE config): the single-room generators
+// are not compiled in, which keeps the kernel's code and register allocation to the multi path.
+template <int NW, bool EXT, bool MULTI = false>
 __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
     const int S = G.S;
     {   // Grid(W, H) of None + wall_rect(0, 0, W, H); the row is 4-B aligned in LDS
@@ -1106,7 +1108,9 @@ __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
     G.dn.clear();
     G.ax = -1; G.ay = -1; G.adir = 0; G.nobjs = 0; G.tmask = 0;
     GSTAMP(G, 9);                                                 // attempt setup (mt_sync, grid clear)
-    const int cmd = G.problem == 0 ? gen_multi(G) : gen_single<NW, EXT>(G);
+    int cmd;
+    if constexpr (MULTI) cmd = gen_multi(G);
+    else cmd = G.problem == 0 ? gen_multi(G) : gen_single<NW, EXT>(G);
     if (G.abort) return;
     if (EXT && G.n_obstacles) {
         place_obstacles(G);

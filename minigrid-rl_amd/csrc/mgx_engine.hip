@@ -1103,7 +1103,7 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
 // off the step kernel's critical path.  Episodes are generated in exactly the
 // order the env will consume them, so RNG streams advance as in the reference.
 // One wave per workgroup; all LDS is lane-private (grid row + MT window + objs).
-template <int NW, bool EXT>
+template <int NW, bool EXT, bool MULTI>
 __device__ __forceinline__ void refill_body(const KParams &p) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int tid = threadIdx.x;
@@ -1112,6 +1112,10 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     uint8_t *s_scr = smem + ((64 * p.GSL + 15) & ~15);        // [64] windows + objs
     unsigned long long maxcur = 0;
     uint32_t err = 0;
+#ifdef MGX_REFILL_CLOCK
+    const unsigned long long rc0 = __builtin_amdgcn_s_memtime();   // diagnostics: wave clocks per launch
+    int rc_iters = 0;
+#endif
     if (e < p.n) {
         // The step kernel may be popping this env's ring concurrently: `head` can be stale
         // (older, smaller), which only under-estimates the free slots.
@@ -1137,11 +1141,14 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
             // episode of this epoch's production (unless the invariant needs it), not the wave an
             // extra round -- the retry then continues in the next epoch, its count carried in aux.
             while (nfree > 0) {
+#ifdef MGX_REFILL_CLOCK
+                rc_iters++;
+#endif
                 ResetOut R;
                 G.astart = G.cur;
                 G.abort = false;
                 mt_sync(G);
-                gen_attempt<NW, EXT>(G, R);
+                gen_attempt<NW, EXT, MULTI>(G, R);
                 if (G.nobjs > p.obj_cap) G.err |= 8u;
                 if (G.abort && ++livelocks <= 100000) {
                     if (nfree > nmin) nfree--;
@@ -1179,7 +1186,17 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         unsigned long long o = __shfl_down(maxcur, off);
         maxcur = o > maxcur ? o : maxcur;
         err |= __shfl_down(err, off);
+#ifdef MGX_REFILL_CLOCK
+        rc_iters = max(rc_iters, __shfl_down(rc_iters, off));
+#endif
     }
+#ifdef MGX_REFILL_CLOCK
+    if (tid == 0) {
+        atomicAdd(&p.counters[26], __builtin_amdgcn_s_memtime() - rc0);   // wave clocks
+        atomicAdd(&p.counters[27], (unsigned long long)rc_iters);          // attempt rounds (busiest lane)
+        atomicAdd(&p.counters[28], 1ull);                                  // waves
+    }
+#endif
     if (tid == 0) {
         if (maxcur) {
             ulonglong4 b = p.blk[2 * p.nblk + blockIdx.x];
@@ -1191,12 +1208,19 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
 }
 
 template <int NW, bool EXT>
-__global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) { refill_body<NW, EXT>(p); }
+__global__ __launch_bounds__(64) void mgx_refill_kernel(KParams p) { refill_body<NW, EXT, false>(p); }
 // The default variant (S <= 8, no EXT features) runs beside three step workgroups per CU:
 // 176 + 3 x 112 VGPRs per SIMD lane fill the 512-entry file exactly.
 template <>
 __global__ __launch_bounds__(64, 3) void mgx_refill_kernel<1, false>(KParams p) {
-    refill_body<1, false>(p);
+    refill_body<1, false, false>(p);
+}
+// problem 'multi' without EXT features (every BASELINE config): the multi generator alone
+template <int NW>
+__global__ __launch_bounds__(64) void mgx_refill_multi_kernel(KParams p) { refill_body<NW, false, true>(p); }
+template <>
+__global__ __launch_bounds__(64, 3) void mgx_refill_multi_kernel<1>(KParams p) {
+    refill_body<1, false, true>(p);
 }
 
 // ============================================================== scene kernel
@@ -1636,6 +1660,8 @@ struct mgx_handle {
     bool seed_pending;      // mgx_set_seed called since the last reset
     bool in_flight;         // a refill forked and not yet joined
     bool serial_refill;     // diagnostics (env MGX_SERIAL_REFILL=1): refill on the caller's stream
+    bool refill_multi;      // problem 'multi' without EXT features refills with mgx_refill_multi_kernel
+                            // (env MGX_REFILL_GENERIC=1: the all-problems kernel, for A/B checks)
     hipStream_t side;       // refill stream
     hipEvent_t ev_fork, ev_done;
     void *allocs[16];
@@ -1740,6 +1766,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         h->serial_refill = sv && sv[0] == '1';
         const char *st = std::getenv("MGX_STEP_PRIO");
         h->kp.step_prio = st ? std::atoi(st) : 0;
+        const char *rg = std::getenv("MGX_REFILL_GENERIC");
+        h->refill_multi = !(rg && rg[0] == '1');
     }
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 24;
     h->cfg.mt_table_words = (h->cfg.mt_table_words + MT_FIELDS - 1) / MT_FIELDS * MT_FIELDS;
@@ -1904,6 +1932,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     MGX_SET_LDS(mgx_reset_kernel, h->lds_reset);
     h->lds_refill = (size_t)((64 * (GS + 4) + 15) & ~15) + (size_t)64 * scratch_per_env(p.obj_stride);
     MGX_SET_LDS(mgx_refill_kernel, h->lds_refill);
+    MGX_SET_LDS1(mgx_refill_multi_kernel<1>, h->lds_refill); MGX_SET_LDS1(mgx_refill_multi_kernel<2>, h->lds_refill);
+    MGX_SET_LDS1(mgx_refill_multi_kernel<4>, h->lds_refill);
     MGX_SET_LDS(mgx_fixup_kernel, h->lds_refill);
     MGX_SET_LDS(mgx_scene_kernel, h->lds_refill);
 #undef MGX_SET_LDS
@@ -1952,7 +1982,14 @@ static mgx_status launch_refill(mgx_handle *h, void *stream) {
     if (h->kp.D == 0) return MGX_OK;
     h->refill_launches++;
     const int64_t nblk = (h->kp.n + 63) / 64;
-    MGX_GEN_LAUNCH(mgx_refill_kernel, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp);
+    if (h->refill_multi && !h->ext && h->kp.problem == MGX_PROBLEM_MULTI) {
+        const dim3 g((unsigned)nblk), b(64);
+        if (h->nw == 1) hipLaunchKernelGGL((mgx_refill_multi_kernel<1>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
+        else if (h->nw == 2) hipLaunchKernelGGL((mgx_refill_multi_kernel<2>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
+        else hipLaunchKernelGGL((mgx_refill_multi_kernel<4>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
+    } else {
+        MGX_GEN_LAUNCH(mgx_refill_kernel, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp);
+    }
     HIP_TRY(hipGetLastError());
     return MGX_OK;
 }
