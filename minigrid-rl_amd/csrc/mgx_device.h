@@ -321,6 +321,12 @@ struct Gen {
 #define GCOUNT(G, k) do { } while (0)
 #endif
 
+// Diagnostics only (timing by elimination; episodes are then NOT the reference's): skip generator
+// sections, bit 1 keys + objects, 2 door positions, 4 goal + agent, 8 walls + door draws.
+#ifndef MGX_GEN_SKIP
+#define MGX_GEN_SKIP 0
+#endif
+
 template <int NW>
 __device__ __forceinline__ void put(Gen<NW> &G, int x, int y, uint8_t code) {   // grid.set(x, y, obj)
     const int b = y * G.S + x;
@@ -415,8 +421,8 @@ __device__ __forceinline__ int randbelow_c(Gen<NW> &G, const RbConst K) {
     const uint32_t sh = K.sh;
     for (;;) {
         GCOUNT(G, 21);
-        const int o6 = 6 * G.go;
-        const uint64_t f = ((G.ga >> o6) | (o6 ? G.gb << (60 - o6) : 0ull)) & MT_LOW60;  // words cur..cur+9
+        const int o6 = (int)__umul24((uint32_t)G.go, 6u);
+        const uint64_t f = ((G.ga >> o6) | (G.gb << (60 - o6))) & MT_LOW60;  // words cur..cur+9
         const uint64_t acc = (c1 - f) & (32ull * MT_REP);   // guard bit of slot i <=> field i < c
         const uint32_t left = G.llw - (uint32_t)(G.cur - G.astart);   // words this attempt may still take
         const int j = acc ? (int)(((uint32_t)__ffsll((long long)acc) - 1u - 5u) * 171u >> 10) : MT_FIELDS;
@@ -438,6 +444,67 @@ __device__ __forceinline__ int randbelow_c(Gen<NW> &G, const RbConst K) {
         if (j < MT_FIELDS) return r;
     }
 }
+// consume m <= 10 words of the register queue
+template <int NW>
+__device__ __forceinline__ void mt_advance(Gen<NW> &G, int m) {
+    G.cur += (uint64_t)m;
+    G.go += m;
+    if (G.go >= MT_FIELDS) {
+        G.go -= MT_FIELDS;
+        G.ga = G.gb;
+        G.gb = G.gc;
+        G.gc = win_group(G, div10(G.cur) + 2);
+    }
+}
+// The reference's rejection loop `while True: x = randint(x0, x1); y = randint(y0, y1);
+// if ok(x, y): break` (two _randbelow per draw) with the rejected cells as a bit set.  One SWAR
+// pass over the next ten words finds every complete draw they hold: x is the first word passing
+// x's test, y the first after it passing y's, the next x the first after that...  so a rejected
+// draw costs a few bit operations instead of two randbelow calls.  A draw that straddles the
+// ten words is taken word by word (randbelow_c).  Word consumption and the live-lock cap are
+// exactly randbelow's: the attempt is abandoned when a draw would need a word past the cap.
+template <int NW>
+__device__ __forceinline__ void draw_cell(Gen<NW> &G, const RbConst KX, const RbConst KY, const Bits<NW> &bad, int x0,
+                                          int y0, int &x, int &y) {
+    constexpr uint64_t GM = 32ull * MT_REP;              // guard bit of every slot
+#pragma unroll 1
+    for (;;) {
+        GCOUNT(G, 21);
+        const int o6 = (int)__umul24((uint32_t)G.go, 6u);
+        const uint64_t f = ((G.ga >> o6) | (G.gb << (60 - o6))) & MT_LOW60;   // words cur..cur+9
+        const uint64_t accx = (KX.c1 - f) & GM, accy = (KY.c1 - f) & GM;    // slot passes x's / y's test
+        uint64_t avail = GM;                             // slots not consumed by an earlier candidate
+        int used = 0;                                    // words through the last candidate examined
+        bool ok = false;
+#pragma unroll 1
+        for (;;) {
+            const uint64_t cx = accx & avail;
+            if (!cx) break;
+            const int bx = __ffsll((long long)cx) - 1;                   // guard bit 6 jx + 5
+            const uint64_t cy = accy & avail & ~((2ull << bx) - 1ull);
+            if (!cy) break;
+            const int by = __ffsll((long long)cy) - 1;
+            x = x0 + (int)(((uint32_t)(f >> (bx - 5)) & 31u) >> KX.sh);
+            y = y0 + (int)(((uint32_t)(f >> (by - 5)) & 31u) >> KY.sh);
+            used = (int)((uint32_t)(by + 1) * 171u >> 10);               // jy + 1
+            avail &= ~((2ull << by) - 1ull);
+            if (!bad.test(y * G.S + x)) { ok = true; break; }
+        }
+        const uint32_t left = G.llw - (uint32_t)(G.cur - G.astart);
+        if ((uint32_t)used > left) {                     // a draw would pass the cap
+            G.cur = G.astart + G.llw;
+            G.abort = true;
+            return;
+        }
+        mt_advance(G, used);
+        if (ok) return;
+        x = x0 + randbelow_c(G, KX);                     // the draw across the window's end
+        y = y0 + randbelow_c(G, KY);
+        if (G.abort) return;
+        if (!bad.test(y * G.S + x)) return;
+    }
+}
+
 template <int NW>
 __device__ __forceinline__ int randint(Gen<NW> &G, int a, int b) { return a + randbelow(G, (uint32_t)(b - a + 1)); }
 template <int NW>
@@ -705,6 +772,7 @@ __device__ const int MULTI_TYPES[3] = {T_KEY, T_BALL, T_BOX};
 template <int NW>
 __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     const int S = G.S, mid = S / 2;
+    if (MGX_GEN_SKIP & 8) { G.ax = 1; G.ay = 1; put(G, S - 2, S - 2, CODE_GOAL); add_obj(G, T_GOAL, 15, S - 2, S - 2); return; }
     for (int i = 1; i < S - 1; i++) put(G, mid, i, CODE_WALL);
     if (nr == 3) for (int i = 1; i < mid; i++) put(G, i, mid, CODE_WALL);
     if (nr == 4) for (int i = 1; i < S - 1; i++) put(G, i, mid, CODE_WALL);
@@ -726,7 +794,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     if (G.abort) return;
     // door positions (custom_env.py:646-650, 911-930, 1365-1391)
 #pragma unroll 1
-    for (int d = 0; d < ndoors; d++) {
+    for (int d = 0; d < ((MGX_GEN_SKIP & 2) ? 0 : ndoors); d++) {
         bool horiz; int lo, hi;
         door_geom(nr, d, mid, S, horiz, lo, hi);
         const int v = randint(G, lo, hi);
@@ -739,8 +807,12 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     GSTAMP(G, 12);                                               // door positions
     if (G.abort) return;
     int gx, gy;
-    place_goal_multi(G, gx, gy);
-    place_agent(G);
+    if (MGX_GEN_SKIP & 4) {
+        gx = 1; gy = 1; put(G, gx, gy, CODE_GOAL); add_obj(G, T_GOAL, 15, gx, gy); G.ax = S - 2; G.ay = S - 2;
+    } else {
+        place_goal_multi(G, gx, gy);
+        place_agent(G);
+    }
     GSTAMP(G, 13);                                               // goal + agent (PCG64)
     const int gr = room_of(nr, gx, gy, mid), ar = room_of(nr, G.ax, G.ay, mid);
     // object counters: c0 = (left | upper-left), c1 = (right | lower-left, unused by Q1), c2, c3
@@ -780,8 +852,12 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     // is the tight inner loop: the cells a placement must avoid are one precomputed bit set,
     // so a rejected draw costs two SWAR randbelow and one bit test -- the lanes that need many
     // draws (the wave waits for them) no longer re-run the task set-up per draw.
+    uint64_t reps = 0;                       // bit y*S of every row y (S <= 8): room masks by multiply
+    if (NW == 1)
+        for (int i = 0; i < S; i++) reps |= 1ull << (i * S);
     int r = 0, phase = 0, kleft = 0, kx = -1, ky = -1;
-    bool fin = false;
+    bool fin = (MGX_GEN_SKIP & 1) != 0;
+    if (fin) return;
 #pragma unroll 1
     for (int it = 0; it < 12; it++) {            // advance to the first task (bounded)
         if (phase == 0) { if ((keymask >> (2 * r)) & 1) break; phase = 1; }
@@ -807,9 +883,6 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
             cname = di & 7;
             kib = (di >> 4) & 1;
             if (phase == 1) { ox = kx; oy = ky; }
-            if (!rect_has_free(G, x0, x1, y0, y1, false, gx, gy, chk ? G.ax : -1, chk ? G.ay : -1, ox, oy)) {
-                live_lock(G); return;
-            }
         } else {
             if (oc == 0) { G.err |= 8u; break; }
             const int b = mask_choice(G, oc);
@@ -817,7 +890,6 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
             oc &= ~(1u << b);
             ot = MULTI_TYPES[b / 6];
             cname = b % 6;
-            if (!rect_has_free(G, x0, x1, y0, y1, true, G.ax, G.ay, -1, -1, -1, -1)) { live_lock(G); return; }
         }
         // cells this placement rejects: key -> goal, [agent], [the other key], next to a door;
         // object -> occupied, agent, next to a door
@@ -832,14 +904,18 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
             bad.set(ey0 * S + ex0);
             if (ex1 >= 0) bad.set(ey1 * S + ex1);
             if (ox >= 0) bad.set(oy * S + ox);
-#pragma unroll 1
-            for (;;) {                            // satisfiable (checked above): ends, or hits the word cap
-                GCOUNT(G, 21);
-                x = x0 + randbelow_c(G, kx_);
-                y = y0 + randbelow_c(G, ky_);
-                if (G.abort) return;
-                if (!bad.test(y * S + x)) break;
+            // no acceptable cell in the room: the reference's loop never ends -> live-lock policy
+            // at once (same end state as after the word cap)
+            bool sat;
+            if constexpr (NW == 1) {
+                const uint64_t rows = reps & (((1ull << ((y1 + 1) * S)) - 1ull) & ~((1ull << (y0 * S)) - 1ull));
+                sat = ((rows * (uint64_t)(((1u << (x1 - x0 + 1)) - 1u) << x0)) & ~bad.w0) != 0;
+            } else {
+                sat = rect_has_free(G, x0, x1, y0, y1, !is_key, ex0, ey0, ex1, ey1, ox, oy);
             }
+            if (!sat) { live_lock(G); return; }
+            draw_cell(G, kx_, ky_, bad, x0, y0, x, y);
+            if (G.abort) return;
         } else {
             int rej = 0;
 #pragma unroll 1
