@@ -643,19 +643,6 @@ __device__ __forceinline__ void place_objects(Gen<NW> &G, uint32_t &oc, const in
     }
 }
 
-// `while True: goal_pos = place_obj(Goal()); if next2door: grid.set(None); continue`
-template <int NW>
-__device__ __forceinline__ void place_goal_multi(Gen<NW> &G, int &gx, int &gy) {
-    for (uint32_t it = 0;; ++it) {
-        if (it > PCG_LOOP_LIMIT) { G.err |= 4u; break; }
-        draw_free_cell(G, gx, gy);
-        if (next2door(G, gx, gy)) continue;      // placed then removed: net no-op
-        break;
-    }
-    put(G, gx, gy, CODE_GOAL);
-    add_obj(G, T_GOAL, 15, gx, gy);
-}
-
 __device__ __forceinline__ int door_code(int cname, bool locked, bool open) {
     return open ? mk_code(T_OPEN, cn2idx(cname), 0) : mk_code(T_DOOR, cn2idx(cname), locked ? 1 : 0);
 }
@@ -806,12 +793,31 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     }
     GSTAMP(G, 12);                                               // door positions
     if (G.abort) return;
-    int gx, gy;
+    int gx = 1, gy = 1;
     if (MGX_GEN_SKIP & 4) {
         gx = 1; gy = 1; put(G, gx, gy, CODE_GOAL); add_obj(G, T_GOAL, 15, gx, gy); G.ax = S - 2; G.ay = S - 2;
     } else {
-        place_goal_multi(G, gx, gy);
-        place_agent(G);
+        // `while True: goal_pos = place_obj(Goal()); if next2door: grid.set(None); continue` then
+        // place_agent() (custom_env.py:653-667, 933-947, 1394-1408) as ONE
+        // rejection loop: a lane's draws go to the goal until one is accepted (free, not next to
+        // a door), then to the agent (free).  Each lane draws exactly the reference's sequence;
+        // the wave no longer waits for its slowest goal before any lane places its agent.
+        bool agent = false;
+#pragma unroll 1
+        for (uint32_t it = 0;; ++it) {
+            GCOUNT(G, 22);
+            if (it > 2 * PCG_LOOP_LIMIT) { G.err |= 4u; G.ax = 1; G.ay = 1; break; }
+            const int x = pcg_integers(G.pcg, 0, S);
+            const int y = pcg_integers(G.pcg, 0, S);
+            if (occupied(G, y * S + x)) continue;          // (the agent is not placed yet: G.ax = -1)
+            if (agent) { G.ax = x; G.ay = y; break; }
+            if (next2door(G, x, y)) continue;              // goal placed then removed: net no-op
+            gx = x; gy = y;
+            put(G, gx, gy, CODE_GOAL);
+            add_obj(G, T_GOAL, 15, gx, gy);
+            agent = true;
+        }
+        G.adir = pcg_integers(G.pcg, 0, 4);
     }
     GSTAMP(G, 13);                                               // goal + agent (PCG64)
     const int gr = room_of(nr, gx, gy, mid), ar = room_of(nr, G.ax, G.ay, mid);

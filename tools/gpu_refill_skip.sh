@@ -7,7 +7,7 @@ O=$R/gpurun_out
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 export MGX_SERIAL_REFILL=1
-for k in "" 1 2 4 8; do
+for k in ${SKIPS:-"" 1 2 4 8}; do
   L=$R/minigrid-rl_amd/mgx/libmgx${k:+_skip$k}.so
   MGX_LIB_PATH=$L timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/skip$k -o run --output-format csv -- python3 $R/tools/refill_cost.py > $O/skip$k.log 2>&1 || { tail -20 $O/skip$k.log; exit 1; }
   python3 -c "
