@@ -463,10 +463,11 @@ __device__ __forceinline__ void mt_advance(Gen<NW> &G, int m) {
 // draw costs a few bit operations instead of two randbelow calls.  A draw that straddles the
 // ten words is taken word by word (randbelow_c).  Word consumption and the live-lock cap are
 // exactly randbelow's: the attempt is abandoned when a draw would need a word past the cap.
-template <int NW>
-__device__ __forceinline__ void draw_cell(Gen<NW> &G, const RbConst KX, const RbConst KY, const Bits<NW> &bad, int x0,
-                                          int y0, int &x, int &y) {
+template <int NW, typename Bad, typename Sat>
+__device__ __forceinline__ void draw_cell(Gen<NW> &G, const RbConst KX, const RbConst KY, int x0, int y0, int &x, int &y,
+                                          Bad bad, Sat sat /* probe after SAT_PROBE rejections; null: none */) {
     constexpr uint64_t GM = 32ull * MT_REP;              // guard bit of every slot
+    int rej = 0;
 #pragma unroll 1
     for (;;) {
         GCOUNT(G, 21);
@@ -488,7 +489,8 @@ __device__ __forceinline__ void draw_cell(Gen<NW> &G, const RbConst KX, const Rb
             y = y0 + (int)(((uint32_t)(f >> (by - 5)) & 31u) >> KY.sh);
             used = (int)((uint32_t)(by + 1) * 171u >> 10);               // jy + 1
             avail &= ~((2ull << by) - 1ull);
-            if (!bad.test(y * G.S + x)) { ok = true; break; }
+            if (!bad(x, y)) { ok = true; break; }
+            if (++rej == SAT_PROBE && !sat()) { live_lock(G); return; }
         }
         const uint32_t left = G.llw - (uint32_t)(G.cur - G.astart);
         if ((uint32_t)used > left) {                     // a draw would pass the cap
@@ -501,7 +503,8 @@ __device__ __forceinline__ void draw_cell(Gen<NW> &G, const RbConst KX, const Rb
         x = x0 + randbelow_c(G, KX);                     // the draw across the window's end
         y = y0 + randbelow_c(G, KY);
         if (G.abort) return;
-        if (!bad.test(y * G.S + x)) return;
+        if (!bad(x, y)) return;
+        if (++rej == SAT_PROBE && !sat()) { live_lock(G); return; }
     }
 }
 
@@ -920,28 +923,23 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
                 sat = rect_has_free(G, x0, x1, y0, y1, !is_key, ex0, ey0, ex1, ey1, ox, oy);
             }
             if (!sat) { live_lock(G); return; }
-            draw_cell(G, kx_, ky_, bad, x0, y0, x, y);
+            draw_cell(G, kx_, ky_, x0, y0, x, y, [&](int cx, int cy) { return bad.test(cy * S + cx); },
+                      [] { return true; });
             if (G.abort) return;
         } else {
-            int rej = 0;
-#pragma unroll 1
-            for (;;) {
-                GCOUNT(G, 21);
-                x = x0 + randbelow_c(G, kx_);
-                y = y0 + randbelow_c(G, ky_);
-                if (G.abort) return;
-                const bool bad = (x == ex0 && y == ey0) || (x == ex1 && y == ey1) || (x == ox && y == oy) ||
-                                 (!is_key && occupied(G, y * S + x)) || next2door(G, x, y);
-                if (!bad) break;
-                if (++rej == SAT_PROBE) {            // provably unsatisfiable loop -> live-lock policy
-                    bool sat = false;
-                    for (int xx = x0; xx <= x1 && !sat; xx++)
-                        for (int yy = y0; yy <= y1 && !sat; yy++)
-                            sat = !((xx == ex0 && yy == ey0) || (xx == ex1 && yy == ey1) || (xx == ox && yy == oy) ||
-                                    (!is_key && occupied(G, yy * S + xx)) || next2door(G, xx, yy));
-                    if (!sat) { live_lock(G); return; }
-                }
-            }
+            // S > 11: the cells are tested in the LDS grid; after SAT_PROBE rejections an exhaustive
+            // scan of the room decides whether the loop can end (else the live-lock policy)
+            const auto bad = [&](int cx, int cy) {
+                return (cx == ex0 && cy == ey0) || (cx == ex1 && cy == ey1) || (cx == ox && cy == oy) ||
+                       (!is_key && occupied(G, cy * S + cx)) || next2door(G, cx, cy);
+            };
+            draw_cell(G, kx_, ky_, x0, y0, x, y, bad, [&] {
+                for (int xx = x0; xx <= x1; xx++)
+                    for (int yy = y0; yy <= y1; yy++)
+                        if (!bad(xx, yy)) return true;
+                return false;
+            });
+            if (G.abort) return;
         }
         GSTAMP(G, 18);                                           // inner rejection loop
         // commit the placement, then advance to the next task
