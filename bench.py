@@ -384,7 +384,8 @@ def measure_rollout(args, layout, world, rank, dev):
     else:
         for t in range(W):
             eng.step(actions[t])
-    torch.cuda.synchronize(dev)
+    eng.join()                                           # the warm-up's last refill: joined outside the
+    torch.cuda.synchronize(dev)                          # captures (no cross-capture dependency)
     assert eng.calls % E == 0                            # the timed region starts on an epoch boundary
 
     def chunk(c):
@@ -397,10 +398,10 @@ def measure_rollout(args, layout, world, rank, dev):
         else:
             for j in range(H):
                 eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
-        if not aligned:
-            eng.join()                                   # an epoch may still be forked: the chunk's graph
-                                                         # must be self-contained, and the region pays for it
         gae_dones(rew, vals, dones, last_v, gamma, lam, stats=st, out=(adv, ret))
+        eng.join()                                       # the epoch's refill (it ran beside GAE): the
+                                                         # chunk's graph is self-contained, and the region
+                                                         # pays for every refill it forked
 
     nchunks = K // H
     graphs = []
@@ -416,6 +417,11 @@ def measure_rollout(args, layout, world, rank, dev):
                 chunk(c)
                 gr.capture_end()
                 graphs.append(gr)
+        # one untimed replay of each graph (more warm-up steps: every graph is whole refill epochs
+        # ending in a join): the first launch of an instantiated graph pays its upload, ~0.1 ms
+        # that a 20-step window would otherwise count as 5 us per step
+        for gr in graphs:
+            gr.replay()
         torch.cuda.synchronize(dev)
     st0 = eng.stats()
     # refill launches inside the timed region: the forks the steps enqueued (captured once in the
@@ -512,7 +518,7 @@ def measure_rollout(args, layout, world, rank, dev):
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
-            "warmup": W,
+            "warmup": W + (K if graphs else 0),          # + one untimed replay of the graphs
             "warmup_requested": args.warmup,
             "ms_per_step": wall_max * 1e3 / K,
             "higher_is_better": True,

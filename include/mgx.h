@@ -143,10 +143,11 @@ mgx_status mgx_set_seed(mgx_handle *h, int64_t seed);
 /* One vectorised step.  actions_dev: [N] int32 (action_bytes = 4) or int64 (8).
  * Episode pre-generation runs CONCURRENTLY with the steps on a handle-owned
  * side stream, in epochs of K = refill_every calls: the first call of an epoch
- * forks the refill off `stream` (after publishing the previous epoch's
- * episodes), the last call joins it back into `stream`.  The launch sequence
- * depends only on the call count; a stream capture (hipGraph) that covers a
- * whole number of epochs is self-contained (else end it with mgx_join). */
+ * joins the previous epoch's refill into `stream`, publishes its episodes and
+ * forks the next refill off `stream`.  Whatever the caller enqueues between two
+ * epochs (GAE, the policy) overlaps the refill's tail.  The launch sequence
+ * depends only on the call count; end a stream capture (hipGraph) with mgx_join
+ * to make it self-contained. */
 mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes,
                     const mgx_step_out *out, void *stream);
 

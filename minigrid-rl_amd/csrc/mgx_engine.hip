@@ -2006,6 +2006,10 @@ static mgx_status join_refill(mgx_handle *h, void *stream) {
 // refill onto the side stream.  It writes only slots the step kernel cannot pop
 // before the next publish, and RNG state only the refill uses.
 static mgx_status fork_refill(mgx_handle *h, void *stream) {
+    // the previous epoch's refill is joined here, not at that epoch's last step: work the caller
+    // enqueues between epochs (GAE, the policy forward) runs beside the refill's tail
+    mgx_status js = join_refill(h, stream);
+    if (js != MGX_OK) return js;
     HIP_TRY(hipMemcpyAsync(h->kp.ring_pub, h->kp.ring_tail, (size_t)h->kp.n, hipMemcpyDeviceToDevice,
                            (hipStream_t)stream));
     if (h->serial_refill) return launch_refill(h, stream);
@@ -2117,7 +2121,6 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
         HIP_TRY(hipGetLastError());
     }
     h->calls++;
-    if (h->kp.D > 0 && h->calls % (uint64_t)h->refill_every == 0) return join_refill(h, stream);
     return MGX_OK;
 }
 
@@ -2156,7 +2159,6 @@ mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_b
                            (hipStream_t)stream, h->kp, o, (const int64_t *)actions_dev);
     HIP_TRY(hipGetLastError());
     h->calls++;
-    if (h->calls % (uint64_t)h->refill_every == 0) return join_refill(h, stream);
     return MGX_OK;
 }
 

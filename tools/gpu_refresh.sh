@@ -21,6 +21,8 @@ import csv
 for r in list(csv.DictReader(open('$O/prof/run_kernel_stats.csv')))[:6]:
     print(r['Name'][:70], r['Calls'], r['AverageNs'], r['Percentage'])
 "
+# refill kernel alone (serial on the caller's stream), BASELINE config 2 shape
+MGX_SERIAL_REFILL=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_serial -o run --output-format csv -- python3 $R/tools/refill_cost.py > $O/prof_serial.log 2>&1 || { tail -20 $O/prof_serial.log; exit 1; }
 P="timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv"
 for L in compact sb3; do
   $P --pmc FETCH_SIZE -d $O/pmcF_$L -o run -- python3 $R/bench.py --layout $L --steps 256 --warmup 64 --cpu-seconds 0 --probe 0 --graph 0 --both-layouts 0 > $O/pmcF_$L.log 2>&1 || { tail -20 $O/pmcF_$L.log; exit 1; }
