@@ -462,6 +462,11 @@ def measure_rollout(args, layout, world, rank, dev):
             cbuf.step(t % H, actions[W + K + t])   # rows are overwritten: timing only
         else:
             eng.step(actions[W + K + t])
+    # the host enqueues the probe's launches one by one (~15 us of Python per step, about the
+    # kernel's own time): a spin kernel first keeps the GPU busy until they are all queued, so
+    # the windows time back-to-back launches, not the host
+    if hasattr(torch.cuda, "_sleep"):
+        torch.cuda._sleep(int(P * 40e-6 * 2.4e9))
     for t in range(P):
         if eng.epoch_boundary():
             if cur is not None:
