@@ -107,3 +107,48 @@ def test_carry_over_and_minibatch_gather():
         for key in ("image", "direction", "mission"):
             want = torch.stack([seen[int(tt)][key][int(ee)] for tt, ee in zip(t_.tolist(), env.tolist())])
             assert torch.equal(got[key], want), key
+
+
+def test_graph_replays_equal_eager_steps():
+    """Refill epochs captured in hipGraphs (whole epochs ending in mgx_join, as bench.py does: the
+    join of each epoch sits at the next epoch's fork, include/mgx.h) replay the same transitions as
+    eager steps: two engines of one config and seed, one stepped eagerly, one by replaying a graph
+    of E steps with the actions copied into its static buffer; rows, rewards, dones and the final
+    engine state must be equal."""
+    _need_gpu()
+    from mgx import MgxEngine
+    from mgx.compact import CompactBuffer
+    n, E, reps = 256, 8, 6
+    kw = dict(problem="multi", mission=None, size=8, n_envs=n, refill_every=E)
+    eager, graphed = MgxEngine(**kw), MgxEngine(**kw)
+    be, bg = CompactBuffer(eager, E), CompactBuffer(graphed, E)
+    eager.reset(); graphed.reset()
+    be.observe(0); bg.observe(0)
+    rng = np.random.default_rng(5)
+    acts = [torch.as_tensor(rng.integers(0, 7, (E, n)), device=eager.device, dtype=torch.int32) for _ in range(reps)]
+    static = torch.zeros((E, n), device=graphed.device, dtype=torch.int32)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        gr = torch.cuda.CUDAGraph()
+        gr.capture_begin()
+        for j in range(E):
+            bg.step(j, static[j])
+        graphed.join()
+        gr.capture_end()
+    torch.cuda.synchronize()
+    for r in range(reps):
+        if r:
+            be.carry_over(); bg.carry_over()
+        for j in range(E):
+            be.step(j, acts[r][j])
+        static.copy_(acts[r])
+        gr.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(be.rows, bg.rows), r
+        assert torch.equal(be.rewards, bg.rewards), r
+        assert torch.equal(be.starts, bg.starts), r
+    de, dg = eager.dump_state(), graphed.dump_state()
+    for k in de:
+        a, b = np.asarray(de[k]), np.asarray(dg[k])
+        assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), k      # None is stored as NaN
