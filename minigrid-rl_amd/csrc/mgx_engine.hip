@@ -770,12 +770,35 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     }
     if (tid < BLOCK_ENVS) {                            // wave 0: ballot compaction of the lists
         const unsigned long long fm = __ballot(fill), dm = __ballot(done), pm = __ballot(popped);
-        const unsigned long long tm = __ballot(tid < ne && s_term[tid]);
+        const unsigned long long tm = __ballot(tid < ne && s_term[tid]), gm = __ballot(dirty);
         if (fill) s_flist[__popcll(fm & __lanemask_lt())] = (uint8_t)tid;
         if (popped) s_dlist[__popcll(pm & __lanemask_lt())] = (uint8_t)tid;
-        if (tid == 0) { s_nf = __popcll(fm); s_nd = __popcll(dm); s_npop = __popcll(pm); s_dmask = dm; s_tmask = tm; }
+        if (tid == 0) {
+            s_nf = __popcll(fm); s_nd = __popcll(dm); s_npop = __popcll(pm); s_dmask = dm; s_tmask = tm;
+            s_dirtym = gm;
+        }
     }
+    if (my_err) atomicOr(p.err, my_err);
     __syncthreads();
+    // ring heads: the popped slot is consumed (its DMA landed in phase 1), so the refill may
+    // reuse it.  Every lane writes its head, changed or not: one 64-B store per block instead
+    // of a byte store per popped env.
+    if (tid < ne && p.D > 0) p.ring_head[e0 + tid] = (uint8_t)(new_head >= 0 ? new_head : rhead);
+    // ---- phase 5 (issued here, before the render, so the stores drain under it): write back
+    // the grids that changed (moves, pickups, resets; a popped env's new grid is in the staging
+    // area, both chunk-major), at line granularity: grids smaller than a 128-B line are written
+    // for every env of a line with a dirty grid, so that no line is written in part.
+    if (!(MGX_DIAG_SKIP & 16)) {
+        const int q16 = p.GS >> 4;
+        const int epl = p.GS < 128 ? 128 / p.GS : 1;          // envs per line (GS is a multiple of 16)
+        const unsigned long long dirtym = s_dirtym;
+        uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * p.GS);
+        for (int i = tid; i < ne * q16; i += BLOCK_THREADS) {
+            const int e = i / q16, c = i - e * q16;
+            if (!((dirtym >> (e & ~(epl - 1))) & ((1ull << epl) - 1))) continue;
+            dst[i] = *reinterpret_cast<const uint4 *>((s_popf[e] ? s_pgrid : s_grid) + c * (BLOCK_ENVS * 16) + e * 16);
+        }
+    }
 
 #ifdef MGX_STAMPS
     tsA = __builtin_amdgcn_s_memtime();
@@ -852,7 +875,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             if (COMPACT && q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);   // row byte 0: direction
         }
     }
-    __syncthreads();
+    // COMPACT without process_vis: each wave copies out the 16 rows it rendered itself (below),
+    // no block barrier -- the waves leave the lock-step here
+    const bool wave_rows = COMPACT && !p.vis;
+    if (!wave_rows) __syncthreads();
     if (p.vis) {                                       // see_through_walls=False: process_vis
         if (tid < ne) apply_vis(s_stk + tid * FSTRIDE + FOFF);
         __syncthreads();
@@ -871,16 +897,6 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             for (int off = q; off < IMG - FRAME; off += 4) t[off] = old[off + FRAME];
         }
     }
-    if (tid < BLOCK_ENVS) {
-        const unsigned long long dm = __ballot(dirty);
-        if (tid == 0) s_dirtym = dm;
-    }
-    if (my_err) atomicOr(p.err, my_err);
-    __syncthreads();
-    // ring heads: the popped slot is consumed (its DMA landed in phase 1), so the refill may
-    // reuse it.  Every lane writes its head, changed or not: one 64-B store per block instead
-    // of a byte store per popped env.
-    if (tid < ne && p.D > 0) p.ring_head[e0 + tid] = (uint8_t)(new_head >= 0 ? new_head : rhead);
 #ifdef MGX_STAMPS
     ts2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -891,14 +907,20 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // after phase 1 and the rest here, so the 128-B lines across each row's seam were written
     // in two halves far apart in time; on MI355X that took 36 us per step instead of 27.
     if (COMPACT) {
-        // the block's rows are contiguous in LDS and in the output: one coalesced copy
-        const int nb16 = (ne * FROW) >> 4;
-        const uint4 *src = reinterpret_cast<const uint4 *>(s_stk);
-        uint4 *dst = reinterpret_cast<uint4 *>(o.img + e0 * (int64_t)FROW);
-        for (int i = tid; i < nb16; i += BLOCK_THREADS) dst[i] = src[i];
-        const int rem = ((ne * FROW) >> 2) - (nb16 << 2);          // trailing dwords (partial block)
-        if (tid < rem)
-            reinterpret_cast<uint32_t *>(dst + nb16)[tid] = reinterpret_cast<const uint32_t *>(src + nb16)[tid];
+        // rows are contiguous in LDS and in the output: coalesced copies, per wave (its 16 rows,
+        // 2,368 B, 16-B aligned) or, after a block barrier, per block
+        const int r0 = wave_rows ? (tid >> 6) * 16 : 0;
+        const int nr = wave_rows ? max(0, min(16, ne - r0)) : ne;
+        const int t = wave_rows ? (tid & 63) : tid, nt = wave_rows ? 64 : BLOCK_THREADS;
+        // this wave's LDS row stores before its own loads of them (other lanes' bytes)
+        if (wave_rows) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const int nb16 = (nr * FROW) >> 4;
+        const uint4 *src = reinterpret_cast<const uint4 *>(s_stk + r0 * FROW);
+        uint4 *dst = reinterpret_cast<uint4 *>(o.img + (e0 + r0) * (int64_t)FROW);
+        for (int i = t; i < nb16; i += nt) dst[i] = src[i];
+        const int rem = ((nr * FROW) >> 2) - (nb16 << 2);          // trailing dwords (partial block)
+        if (t < rem)
+            reinterpret_cast<uint32_t *>(dst + nb16)[t] = reinterpret_cast<const uint32_t *>(src + nb16)[t];
     } else if (fast) {
         // Block-relative output dword k needs old dwords k+36, k+37 (alignbyte by 3) while its
         // env column j = k mod 147 <= 109; dword 110 mixes old byte 587 with new bytes 0..2;
@@ -992,21 +1014,6 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
 #ifdef MGX_STAMPS
     tsC = __builtin_amdgcn_s_memtime();
 #endif
-    // ---- phase 5: write back grids that changed (moves, pickups, resets)
-    // (a popped env's new grid is in the staging area; both chunk-major)
-    // At line granularity: grids smaller than a 128-B line are written for every env of a
-    // line with a dirty grid, so that no line is written in part.
-    if (!(MGX_DIAG_SKIP & 16)) {
-        const int q16 = p.GS >> 4;
-        const int epl = p.GS < 128 ? 128 / p.GS : 1;          // envs per line (GS is a multiple of 16)
-        const unsigned long long dirtym = s_dirtym;
-        uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * p.GS);
-        for (int i = tid; i < ne * q16; i += BLOCK_THREADS) {
-            const int e = i / q16, c = i - e * q16;
-            if (!((dirtym >> (e & ~(epl - 1))) & ((1ull << epl) - 1))) continue;
-            dst[i] = *reinterpret_cast<const uint4 *>((s_popf[e] ? s_pgrid : s_grid) + c * (BLOCK_ENVS * 16) + e * 16);
-        }
-    }
     if (tid == 0) {
         // workgroup-private stats slot: fire-and-forget adds (no load on the kernel's tail)
         atomicAdd(&p.blk[blockIdx.x].x, (unsigned long long)ne);
@@ -1665,6 +1672,7 @@ struct mgx_handle {
     hipStream_t side;       // refill stream
     hipEvent_t ev_fork, ev_done;
     void *allocs[16];
+    uint32_t *scene_dev;    // mgx_scene's record (inside allocs[15], inline mode only)
 };
 
 extern "C" {
@@ -1901,12 +1909,14 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     }
     p.D = D;
     p.start_rng = nullptr;
-    if (D == 0) {   // inline mode: keep each episode's generation start state (mgx_scene)
-        hipError_t e = hipMalloc(&h->allocs[15], (size_t)N * 32);
+    if (D == 0) {   // inline mode: keep each episode's generation start state (mgx_scene) + its record
+        const size_t bytes = (size_t)N * 32 + MGX_SCENE_WORDS * sizeof(uint32_t);
+        hipError_t e = hipMalloc(&h->allocs[15], bytes);
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc start rng"));
-        e = hipMemset(h->allocs[15], 0, (size_t)N * 32);
+        e = hipMemset(h->allocs[15], 0, bytes);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset start rng"));
         p.start_rng = (uint4 *)h->allocs[15];
+        h->scene_dev = (uint32_t *)((char *)h->allocs[15] + (size_t)N * 32);
     }
     p.K = h->cfg.refill_every;
     p.cap = h->cfg.refill_cap;
@@ -2208,16 +2218,12 @@ mgx_status mgx_scene(mgx_handle *h, int64_t env, uint32_t *record, void *stream)
     if (env < 0 || env >= h->kp.n) return fail(MGX_ERR_INVALID, "mgx_scene: env out of range");
     if (!h->kp.start_rng) return fail(MGX_ERR_INVALID, "mgx_scene: needs inline resets (ring_depth = -1)");
     if (h->kp.S * h->kp.S > 4 * (MGX_SCENE_WORDS - 8 - MAX_OBJS)) return fail(MGX_ERR_INVALID, "mgx_scene: grid too large");
-    uint32_t *dev = nullptr;
-    HIP_TRY(hipMalloc(&dev, MGX_SCENE_WORDS * sizeof(uint32_t)));
+    uint32_t *dev = h->scene_dev;                 // handle-owned record (inline mode allocates it)
     HIP_TRY(hipMemsetAsync(dev, 0, MGX_SCENE_WORDS * sizeof(uint32_t), (hipStream_t)stream));
     MGX_GEN_LAUNCH(mgx_scene_kernel, dim3(1), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, env, dev);
-    hipError_t le = hipGetLastError();
-    hipError_t ce = le == hipSuccess ? hipMemcpyAsync(record, dev, MGX_SCENE_WORDS * sizeof(uint32_t),
-                                                      hipMemcpyDeviceToHost, (hipStream_t)stream) : le;
-    hipError_t se = ce == hipSuccess ? hipStreamSynchronize((hipStream_t)stream) : ce;
-    (void)hipFree(dev);
-    if (se != hipSuccess) return fail(MGX_ERR_HIP, std::string("mgx_scene: ") + hipGetErrorString(se));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(record, dev, MGX_SCENE_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     return MGX_OK;
 }
 
