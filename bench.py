@@ -451,10 +451,12 @@ def measure_rollout(args, layout, world, rank, dev):
     gpu_ms = ev0.elapsed_time(ev1)
     st1 = eng.stats()
     eng.poll_error()
-    # roofline probe: per-launch duration of mgx_step_kernel (HIP events on its stream)
-    # Windows of consecutive launches that neither fork nor join a refill epoch: each
-    # bracketed by one event pair, so the per-launch figure is kernel time plus the
-    # back-to-back dispatch gap (no host latency in it).
+    # roofline probe: per-launch duration of mgx_step_kernel (HIP events on its stream) in the
+    # timed region's regime.  Whole refill epochs; each window is an epoch's launches after its
+    # first (the first joins the previous epoch's refill and forks the next), bracketed by one
+    # event pair, so the per-launch figure is kernel time plus the back-to-back dispatch gap, with
+    # the refill beside the steps for as long as it runs (an event pair around every launch would
+    # keep consecutive launches from overlapping at all).
     windows, cur = [], None
 
     def probe_step(t):
@@ -483,6 +485,7 @@ def measure_rollout(args, layout, world, rank, dev):
     if cur is not None:
         cur[1].record(stream)
         windows.append(cur)
+    eng.join()
     torch.cuda.synchronize(dev)
     eng.poll_error()
     probe_us = []

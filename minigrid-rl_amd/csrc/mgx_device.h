@@ -322,7 +322,8 @@ struct Gen {
 #endif
 
 // Diagnostics only (timing by elimination; episodes are then NOT the reference's): skip generator
-// sections, bit 1 keys + objects, 2 door positions, 4 goal + agent, 8 walls + door draws.
+// sections, bit 1 keys + objects, 2 door positions, 4 goal + agent, 8 walls + door draws; inside the
+// keys + objects loop: 16 the MT top-up, 32 the object choice draw.
 #ifndef MGX_GEN_SKIP
 #define MGX_GEN_SKIP 0
 #endif
@@ -879,7 +880,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     while (!fin) {
         GCOUNT(G, 20);
         GSTAMP(G, 19);                                           // (commit + task advance of the previous)
-        mt_topup(G);
+        if (!(MGX_GEN_SKIP & 16)) mt_topup(G);
         GSTAMP(G, 16);                                           // MT window top-up
         int x0, x1, y0, y1;
         room_rect(nr, r, mid, S, x0, x1, y0, y1);
@@ -894,7 +895,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
             if (phase == 1) { ox = kx; oy = ky; }
         } else {
             if (oc == 0) { G.err |= 8u; break; }
-            const int b = mask_choice(G, oc);
+            const int b = (MGX_GEN_SKIP & 32) ? __ffs(oc) - 1 : mask_choice(G, oc);
             if (G.abort) return;
             oc &= ~(1u << b);
             ot = MULTI_TYPES[b / 6];

@@ -150,10 +150,10 @@ class MgxEngine:
         return self.obs
 
     def epoch_boundary(self, call=None):
-        """True if step call number `call` (default: the next one) forks or joins a refill."""
+        """True if step call number `call` (default: the next one) starts a refill epoch: it joins
+        the previous epoch's refill and forks the next (include/mgx.h, mgx_step)."""
         c = self.calls if call is None else call
-        K = self.refill_every
-        return self.ring_depth > 0 and (c % K == 0 or (c + 1) % K == 0)
+        return self.ring_depth > 0 and c % self.refill_every == 0
 
     def join(self):
         """Make the current stream wait for the in-flight episode refill (mgx_join)."""
