@@ -91,6 +91,7 @@ struct KParams {
     int initial_fill;       // this refill launch is mgx_reset's (fill every ring to 2K)
     int reset_mode;         // mgx_reset: 0 first (seeded, MT cursor 0), 1 seeded, 2 unseeded
     int step_prio;          // s_setprio of the step kernel's waves (env MGX_STEP_PRIO, 0..3)
+    int prod_mean;          // refill production per lane capped at the wave's mean deficit (env MGX_REFILL_MEAN)
     uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
                             //        generation (mgx_scene regenerates it), else null
 };
@@ -1123,18 +1124,34 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     const unsigned long long rc0 = __builtin_amdgcn_s_memtime();   // diagnostics: wave clocks per launch
     int rc_iters = 0;
 #endif
+    // The step kernel may be popping this env's ring concurrently: `head` can be stale
+    // (older, smaller), which only under-estimates the free slots.
+    uint8_t tail = 0;
+    int level = 0;
     if (e < p.n) {
-        // The step kernel may be popping this env's ring concurrently: `head` can be stale
-        // (older, smaller), which only under-estimates the free slots.
         const uint8_t head = *reinterpret_cast<volatile const uint8_t *>(p.ring_head + e);
-        uint8_t tail = p.ring_tail[e];
-        // Production: at least what keeps >= K episodes queued at the next join (each step
-        // pops <= 1, so 2K - level), plus up to `cap` more while there is room.  Capping the
-        // per-epoch production balances work across the lanes of a wave (its time is the
-        // busiest lane's) while rings with slack absorb bursts of short episodes.
-        const int level = (int)(uint8_t)(tail - head);
-        const int space = p.D - level, need = 2 * p.K - level;
-        int nfree = p.initial_fill ? need : max(need, p.cap < 0 ? space : min(p.cap, space));
+        tail = p.ring_tail[e];
+        level = (int)(uint8_t)(tail - head);
+    }
+    const int space = p.D - level, need = 2 * p.K - level;
+    // Production: at least what keeps >= K episodes queued at the next join (each step pops
+    // <= 1, so 2K - level), plus up to `cap` more while there is room.  Capping the per-epoch
+    // production balances work across the lanes of a wave (its time is the busiest lane's)
+    // while rings with slack absorb bursts of short episodes.  prod_mean: the cap is also the
+    // wave's mean deficit (D - level, rounded), so the wave runs about as many attempt rounds as
+    // its lanes consumed on average, not as many as its busiest lane did; a lane left behind
+    // keeps its deficit, which raises the next epoch's mean (the ring depth absorbs it).
+    int cap = p.cap;
+    if (p.prod_mean && cap > 0 && !p.initial_fill) {
+        int sum = e < p.n ? space : 0, cnt = e < p.n ? 1 : 0;
+        for (int off = 32; off > 0; off >>= 1) {
+            sum += __shfl_xor(sum, off);
+            cnt += __shfl_xor(cnt, off);
+        }
+        cap = min(cap, (2 * sum + cnt) / (2 * max(cnt, 1)));
+    }
+    if (e < p.n) {
+        int nfree = p.initial_fill ? need : max(need, p.cap < 0 ? space : min(cap, space));
         nfree = min(nfree, space);
         int nmin = max(need, 0);                   // what the ring invariant requires this epoch
         if (nfree > 0) {
@@ -1774,6 +1791,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         h->serial_refill = sv && sv[0] == '1';
         const char *st = std::getenv("MGX_STEP_PRIO");
         h->kp.step_prio = st ? std::atoi(st) : 0;
+        const char *pm = std::getenv("MGX_REFILL_MEAN");
+        h->kp.prod_mean = pm ? std::atoi(pm) : 1;
         const char *rg = std::getenv("MGX_REFILL_GENERIC");
         h->refill_multi = !(rg && rg[0] == '1');
     }
