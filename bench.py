@@ -84,8 +84,8 @@ def parse():
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
     ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layout")
     ap.add_argument("--layout", default=None, choices=["compact", "sb3"],
-                    help="observation storage: materialised SB3 stacks (mgx_step; rollout default) or "
-                         "compact rows + mgx_gather (mgx_step_compact; ppo default)")
+                    help="observation storage: compact rows + mgx_gather (mgx_step_compact; the default of "
+                         "both workloads) or the materialised SB3 stacks (mgx_step, the VecEnv drop-in's)")
     args = ap.parse_args()
     presets = {2: dict(mission="5", size=8, n_envs=65536), 4: dict(mission="None", size=8, n_envs=32768),
                5: dict(mission="1", size=16, n_envs=131072)}
@@ -135,7 +135,8 @@ def cpu_baseline(args, seconds):
       config 1   1 process, 1 env, GTG 8x8 (BASELINE configs[0])."""
     import multiprocessing as mp
     mission = None if args.mission == "None" else int(args.mission)
-    P = max(1, min(len(os.sched_getaffinity(0)), 16))
+    affinity = len(os.sched_getaffinity(0))
+    P = max(1, min(affinity, 16))
     ctx = mp.get_context("fork")                           # no GPU state exists yet in this process
     q = ctx.Queue()
     procs = [ctx.Process(target=_cpu_leg, args=(args.problem, mission, args.size, 1, seconds, 7 + i, q))
@@ -152,9 +153,28 @@ def cpu_baseline(args, seconds):
                 sample="C port of the reference env (oracle/mgx_oracle.c orc_bench: object grid, slice+rotate+"
                        "encode per step, tokenised mission, auto-reset), random actions, same config as the GPU "
                        "line; %d processes x 1 env x %.1fs; host: %s" % (P, seconds, _cpu_model()),
+                affinity_cpus=affinity, cpu_count=os.cpu_count(),
+                cap_note="P = min(affinity, 16): the reference's SubprocVecEnv runs n_envs = 16 workers "
+                         "(algorithm/ppo.yaml:4), and a shared GPU box grants 16 CPUs per GPU",
+                reference_python=_reference_cpu(),
                 legs={"all_cores": {"value": all_cores, "processes": P, "envs_per_process": 1},
                       "one_thread": {"value": s1 / t1, "processes": 1, "envs": 1024, "seconds": t1},
                       "config1_gtg8_1env": {"value": c1 / tc1, "processes": 1, "envs": 1, "seconds": tc1}})
+
+
+def _reference_cpu():
+    """The reference's own Python env timed by tools/ref_cpu_bench.py (custom_env.py + environment.py
+    wrappers, unchanged, 1 process x 1 env, GTG 8x8).  /root/reference exists only in the build
+    container, so this leg is recorded there (profiles/r03_reference_cpu.json names that host) and
+    reported here as recorded, not re-timed on the GPU box."""
+    path = os.path.join(ROOT, "profiles", "r03_reference_cpu.json")
+    try:
+        r = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return {"value": r["env_steps_per_s"], "unit": "env-steps/s", "us_per_step": r["us_per_step"], "cores": 1,
+            "kind": "reference", "config": r["config"], "host": r["host"],
+            "source": "profiles/r03_reference_cpu.json (tools/ref_cpu_bench.py, build container)"}
 
 
 def _workload_name(args, mission, n, world):
@@ -528,6 +548,10 @@ def measure_rollout(args, layout, world, rank, dev):
             "steps": K,
             "warmup": W + (K if graphs else 0),          # + one untimed replay of the graphs
             "warmup_requested": args.warmup,
+            "warmup_note": "warm-up raised to >= 2,048 steps in whole refill epochs (+ one untimed replay of "
+                           "each graph): the episode rings fill towards their depth for ~1,500 steps after a "
+                           "reset, and the timed window pays for every episode it consumes (`window`), so a "
+                           "shorter warm-up would time the fill-up instead of the steady state",
             "ms_per_step": wall_max * 1e3 / K,
             "higher_is_better": True,
             "scaling": "weak",
@@ -584,6 +608,10 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    ranks_seen = 1
+    if world > 1:                                     # the collective itself counts the ranks it joined
+        ones = _allreduce(torch.ones(1, dtype=torch.float64, device=dev), dist.ReduceOp.SUM)
+        ranks_seen = int(round(float(ones[0])))
     if args.workload == "ppo":
         return main_ppo(args, world, rank, local, dev)
     out = measure_rollout(args, args.layout, world, rank, dev)
@@ -594,6 +622,8 @@ def main():
         o2 = measure_rollout(args, other, world, rank, dev)
         out[other + "_layout"] = {k: o2[k] for k in ("value", "ms_per_step", "roofline", "window")}
     if rank == 0:
+        out["ranks_seen"] = ranks_seen
+        out["dist_backend"] = dist.get_backend() if world > 1 else None
         if cpu is not None:
             out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MGX_ABI_VERSION 3
+#define MGX_ABI_VERSION 4
 
 /* Live-lock cap (engine policy; the reference hangs): a
  * reset attempt may consume at most this many MT19937 words; the attempt that
@@ -60,7 +60,8 @@ typedef enum {
 typedef enum { MGX_TERMINAL_NONE = 0, MGX_TERMINAL_TRUNCATED = 1, MGX_TERMINAL_ALL = 2 } mgx_terminal_mode;
 
 /* Device error bits reported by mgx_poll_error */
-#define MGX_DEVERR_MT_TABLE   1u   /* an env ran past the MT19937 output table */
+#define MGX_DEVERR_MT_TABLE   1u   /* an env's MT19937 cursor left the window of the stream the device holds
+                                      (live cursors spread over more than mt_table_words) */
 #define MGX_DEVERR_BAD_ACTION 2u   /* action outside 0..6 (minigrid raises ValueError) */
 #define MGX_DEVERR_PCG_LOOP   4u   /* a PCG64 rejection loop exceeded its safety bound */
 #define MGX_DEVERR_OBJECTS    8u   /* generator ran out of objects (AssertionError / IndexError in the reference) */
@@ -86,12 +87,19 @@ typedef struct mgx_config {
     int32_t refill_cap;        /* episodes an env may pre-generate per refill epoch beyond what keeps the
                                   ring from running dry (0 -> max(2, round(0.19 * refill_every)), i.e. 6
                                   at the default epoch; < 0 -> fill the ring) */
-    int64_t mt_table_words;    /* 0 -> default (2^24); shared MT19937 output table length */
+    int64_t mt_table_words;    /* 0 -> default (2^24): MT19937 output words the device keeps (rounded up to a
+                                  power of two of 10-word groups, >= 5,120).  The stream is extended on the
+                                  device as cursors advance -- no lifetime limit; only the spread between
+                                  the oldest live cursor and the newest must stay below it */
     int32_t ring_depth;        /* pre-generated episodes per env (0 -> 128; rounded up to a power of two
                                   <= 128; -1 = no ring: every auto-reset generated inline) */
     int32_t refill_every;      /* steps per refill epoch K (0 -> ring_depth/4; clamped to <= ring_depth/2:
                                   each epoch keeps >= K queued, and a step pops <= 1 episode) */
     double percent_obstacles;  /* `env.percent_obstacles` (single.yaml:28: 0.05); used when obstacles */
+    int32_t manual;            /* PlaygroundEnv(manual=True) (make_env(manual=True), environment.py:10-20):
+                                  a 'done' before the mission is complete is a no-op -- no termination,
+                                  no reset (custom_env.py:319-328 `elif not self.manual`) */
+    int32_t reserved0;         /* 0 */
 } mgx_config;
 
 /* Stacked observation in the layout SB3's VecFrameStack(VecTransposeImage(.))
@@ -205,12 +213,15 @@ mgx_status mgx_get_config(const mgx_handle *h, mgx_config *out);
 /* GAE over a [T][N] f32 rollout (DictRolloutBuffer.compute_returns_and_advantage):
  * episode_starts_dev f32 [T][N], last_values f32 [N], last_dones u8 [N];
  * writes advantages/returns f32 [T][N].  adv_stats_dev (optional, f64 [3]):
- * accumulates (sum A, sum A^2, count) for RCCL advantage-stat reduction (through a per-device
- * shard buffer: calls that pass adv_stats_dev must not run concurrently on two streams). */
+ * accumulates (sum A, sum A^2, count) for RCCL advantage-stat reduction, through per-workgroup
+ * partials in stats_scratch_dev (f64 [MGX_GAE_SCRATCH_WORDS], caller-owned, zeroed before its first
+ * use; every call leaves it zeroed).  Calls that may overlap (two collectors on two streams) pass
+ * scratches of their own; NULL = one device-global scratch (such calls must then not overlap). */
+#define MGX_GAE_SCRATCH_WORDS 512
 mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const float *episode_starts_dev,
                    const float *last_values_dev, const uint8_t *last_dones_dev, int64_t T, int64_t N,
                    float gamma, float gamma_lambda, float *advantages_dev, float *returns_dev,
-                   double *adv_stats_dev, void *stream);
+                   double *adv_stats_dev, double *stats_scratch_dev, void *stream);
 
 /* GAE over the compact rollout layout: dones_dev u8 [T][N] is the `done` output of
  * step t (what mgx_step writes to done_dev), so next_non_terminal(t) = 1 - dones[t]
@@ -218,7 +229,8 @@ mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const floa
  * op order, outputs and adv_stats_dev as mgx_gae; 17 B of traffic per element. */
 mgx_status mgx_gae_dones(const float *rewards_dev, const float *values_dev, const uint8_t *dones_dev,
                          const float *last_values_dev, int64_t T, int64_t N, float gamma, float gamma_lambda,
-                         float *advantages_dev, float *returns_dev, double *adv_stats_dev, void *stream);
+                         float *advantages_dev, float *returns_dev, double *adv_stats_dev,
+                         double *stats_scratch_dev, void *stream);
 
 /* Scene record of env `env`'s current episode, for PlaygroundEnv.llm_description /
  * LLMDescriptionWrapper (environment.py:152-195; manual mode, one env): the episode is

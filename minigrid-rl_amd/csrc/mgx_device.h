@@ -274,8 +274,9 @@ struct Gen {
     Bits<NW> occ;          // cell holds an object (walls, doors, goal, keys, boxes, balls)
     Bits<NW> dn;           // cell is next to a door (custom_env.py:2036-2046)
     // MT19937 shared table + cursor: q0..q3 = table[cur .. cur+3]
-    const uint64_t *table; // packed MT19937 field groups (global)
-    uint64_t tlen;         // groups in the table
+    const uint64_t *table; // packed MT19937 field groups (global ring of rmask+1 groups + mirror pad)
+    uint64_t rmask;        // ring slots - 1 (a power of two): group g lives in slot g & rmask
+    uint64_t tlo, thi;     // groups [tlo, thi) of the stream are in the ring (mgx_mt_slide_kernel)
     uint64_t *win;         // LDS window: packed groups [gbase, gbase + MT_WG)
     uint64_t gbase;        // first group in the window
     uint64_t cur, astart;  // word cursor; first word of the current reset attempt
@@ -335,16 +336,15 @@ __device__ __forceinline__ void put(Gen<NW> &G, int x, int y, uint8_t code) {   
     if (code == CODE_EMPTY) G.occ.unset(b); else G.occ.set(b);
 }
 
-// Refill the lane's LDS window with packed groups [g, g + MT_WG): 16 independent
-// 16-B global loads in flight (one L2/HBM round trip), 32 b64 LDS stores.
+// Refill the lane's LDS window with packed groups [g, g + MT_WG) from ring slot g & rmask (the
+// ring is followed by a mirror of its first MT_PAD slots, so the 16 groups are contiguous): 16
+// independent 16-B global loads in flight (one L2/HBM round trip), 32 b64 LDS stores.
 // Out of line: it is the cold path of every draw site (inlined at each of them it
-// made the generator ~2k instructions larger).  Returns ngroups when the table ran out.
+// made the generator ~2k instructions larger).
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
-__device__ __noinline__ uint64_t mt_refill_cold(const uint64_t *__restrict__ table, uint64_t ngroups, lds_u64 *win,
-                                                uint64_t g) {
-    uint64_t base = g;
-    if (base + MT_WG > ngroups) base = ngroups;          // MGX_DEVERR_MT_TABLE: read the zero pad
-    const uint4 *src = reinterpret_cast<const uint4 *>(table + base);
+constexpr int MT_PAD = MT_WG + 4;   // mirror pad groups after the ring (a window may start in its last slot)
+__device__ __noinline__ void mt_refill_cold(const uint64_t *__restrict__ table, uint64_t slot, lds_u64 *win) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(table + slot);
 #pragma unroll
     for (int h = 0; h < MT_WG / 8; h++) {            // 4 x (4 loads in flight, then 8 LDS stores)
         const uint4 v0 = src[4 * h], v1 = src[4 * h + 1], v2 = src[4 * h + 2], v3 = src[4 * h + 3];
@@ -354,17 +354,17 @@ __device__ __noinline__ uint64_t mt_refill_cold(const uint64_t *__restrict__ tab
         d[4] = (uint64_t)v2.x | ((uint64_t)v2.y << 32); d[5] = (uint64_t)v2.z | ((uint64_t)v2.w << 32);
         d[6] = (uint64_t)v3.x | ((uint64_t)v3.y << 32); d[7] = (uint64_t)v3.z | ((uint64_t)v3.w << 32);
     }
-    return base;
 }
 template <int NW>
 __device__ __forceinline__ uint64_t win_group(Gen<NW> &G, uint64_t g) {
     uint64_t off = g - G.gbase;
     if (off >= MT_WG) {
         GCOUNT(G, 23);
-        G.gbase = mt_refill_cold(G.table, G.tlen, (lds_u64 *)G.win, g);
-        if (G.gbase == G.tlen) G.err |= 1u;
-        off = g - G.gbase;
-        if (off >= MT_WG) off = 0;   // only after MGX_DEVERR_MT_TABLE
+        // groups outside [tlo, thi) are not (or no longer) in the ring: MGX_DEVERR_MT_TABLE
+        if (g < G.tlo || g + MT_WG > G.thi) G.err |= 1u;
+        mt_refill_cold(G.table, g & G.rmask, (lds_u64 *)G.win);
+        G.gbase = g;
+        off = 0;
     }
     return G.win[off];
 }
@@ -379,9 +379,10 @@ __device__ __forceinline__ void mt_topup(Gen<NW> &G) {
     const uint64_t g = div10(G.cur);
     const int64_t used = (int64_t)(g - G.gbase);              // < 0 right after a look-ahead refill
     if (__ballot(used >= MT_WG - MGX_MT_TOPUP)) {
-        if (used >= MT_WG / 2 && g + MT_WG <= G.tlen) {
+        if (used >= MT_WG / 2 && g >= G.tlo && g + MT_WG <= G.thi) {
             GCOUNT(G, 25);
-            G.gbase = mt_refill_cold(G.table, G.tlen, (lds_u64 *)G.win, g);
+            mt_refill_cold(G.table, g & G.rmask, (lds_u64 *)G.win);
+            G.gbase = g;
         }
     }
 #endif

@@ -46,6 +46,26 @@ constexpr int BLOCK_THREADS = 256;
 constexpr int FRAME = 147;                 // 3 x 7 x 7
 constexpr int FRAME_DW4 = 147;             // dwords per env row at n_stack == 4 (588 B)
 constexpr int FROW = 148;                  // LDS frame row (fast roll): byte 0 pad, bytes 1..147 frame
+// MT19937 output ring (every env's CPython `random` is MT19937(seed) -- one shared
+// stream read at per-env cursors, custom_env.py:82).  The ring holds groups [lo, hi) of the packed
+// stream (mgx_device.h: ten 5-bit fields per group); hi * 10 words have been generated and `st` is
+// the generator's state after them (a whole number of 624-word blocks).  No env ever reads below
+// its oldest live cursor again -- the end of its current episode (cur_rng: a later VecEnv.reset()
+// continues from there) or, in inline mode, that episode's start (start_rng: mgx_scene regenerates
+// it) -- so mgx_mt_slide_kernel extends the stream on the device to that minimum plus the ring's
+// size, overwriting dead groups: the stream never runs out (round 2's host-built table of 2^24
+// words lasted ~1.1-1.5 M steps per env).
+struct MtCtl {
+    unsigned long long lo, hi;       // groups of the stream held by the ring
+    unsigned long long span_min;     // min live cursor (words) of the running slide pass, ~0 between passes
+    unsigned int done;               // workgroups of the running pass that have reduced
+    unsigned int pad;
+    uint32_t st[624];                // MT19937 state at word hi * 10 (every output of it consumed)
+};
+constexpr int MT_SB_WORDS = 3120;                         // lcm(624, 10): five MT blocks = 312 whole groups
+constexpr int MT_SB_GROUPS = MT_SB_WORDS / MT_FIELDS;
+constexpr int MT_SLIDE_MAX_SB = 8;                        // super-blocks one slide generates at most (25 k words)
+constexpr int SLIDE_THREADS = 1024, SLIDE_ENVS = 4 * SLIDE_THREADS;
 // LDS bytes per resetting lane: MT window + objs list (obj_stride words, see mgx_create)
 __host__ __device__ constexpr int scratch_per_env(int obj_stride) { return WIN_STRIDE * 4 + obj_stride * 4; }
 
@@ -54,11 +74,13 @@ struct KParams {
     uint8_t *grid;
     uint4 *pcg;        // [N][2]
     uint4 *aux;        // [N]
-    const uint64_t *mt;             // packed MT19937(seed) stream: ten 5-bit fields per group
+    uint64_t *mt;                   // packed MT19937(seed) stream: ten 5-bit fields per group, a ring of
+                                    // mt_mask+1 groups + MT_PAD mirror groups, extended by mgx_mt_slide_kernel
     const uint8_t *mtok;
     unsigned long long *counters;   // [0] steps [1] resets [2] livelocks [3] max cursor
     uint32_t *err;
-    uint64_t tlen;                  // groups
+    uint64_t mt_mask;               // ring slots - 1
+    struct MtCtl *mtc;              // ring window + generator state (device)
     int64_t n;
     int64_t seed_base;              // base_seed + env_index_offset
     int S, GS, GSL, grid_lds, n_stack, img_bytes, stk_lds, stk_step, problem, cfg_mission, num_objects, all_doors_open;
@@ -68,6 +90,7 @@ struct KParams {
     int n_obstacles;        // floor((S-2)^2 * percent_obstacles) when cfg.obstacles (custom_env.py:156)
     int vis;                // see_through_walls == False: Grid.process_vis on every frame
     int has_move;           // the problem can draw 'move' missions: target_range words below are live
+    int manual;             // PlaygroundEnv(manual=True): 'done' ends only a completed mission (custom_env.py:325)
     uint64_t *range_cur;    // [N]     target_range of the current episode (mgx_device.h: move_range)
     uint64_t *ring_range;   // [N][D]  ... of each queued episode
     // pre-generated episode ring (see mgx_refill_kernel)
@@ -245,7 +268,9 @@ __device__ __forceinline__ void load_gen(Gen<NW> &G, const KParams &p, int64_t e
     G.g = g;
     G.S = p.S;
     G.table = p.mt;
-    G.tlen = p.tlen;
+    G.rmask = p.mt_mask;
+    G.tlo = p.mtc->lo;              // uniform: scalar loads; the slider runs between kernels, never during
+    G.thi = p.mtc->hi;
     // lane >= 0: workgroup LDS layout [64 windows][64 objs lists]; lane < 0: one env's private block
     G.win = reinterpret_cast<uint64_t *>(scratch + (lane >= 0 ? lane * (WIN_STRIDE * 4) : 0));
     G.objs = reinterpret_cast<uint32_t *>(scratch + (lane >= 0 ? BLOCK_ENVS * (WIN_STRIDE * 4) + lane * (p.obj_stride * 4)
@@ -629,11 +654,6 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         uint8_t *fp = s_grid + cm_off(tid, fy * S + fx);
         const uint8_t fc = *fp;
         const int ft = fc & 15;
-        // the episode ends (auto-reset) exactly when one of these holds; each implies `spec`,
-        // so the next episode is already in LDS (phase 1c)
-        const bool done_e = (a == A_FORWARD && (ft == T_GOAL || ft == T_LAVA)) || a == A_DONE || sc >= ms;
-        const bool avail = done_e && spec;
-        const bool filling = !COMPACT && !done_e && st.frames < p.n_stack;
         // MiniGridEnv.step (3P), as selects: every action's outcome is computed and the taken
         // one kept (a branch per action made a divergent tree of exec-mask updates -- half of
         // this phase's instructions were SALU mask bookkeeping)
@@ -682,7 +702,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
                           (!has_t & (ta != NONE8) & (a == ta)) |
                           ((st.mission_id >= MID_MOVE) & in_move_range(mrange, ax, ay)));
         const int md1 = hit ? 1 : md0, rs1 = (hit && rs0 < 0) ? sc : rs0;
-        const bool dn = !t0 && a == A_DONE;         // 'done': the stored self.reward, or 0 (not manual)
+        // 'done': the stored self.reward, or 0 -- in manual mode only a completed mission ends
+        const bool dn = !t0 && a == A_DONE && (md1 || !p.manual);
         // reward: reaching the goal pays 1 - 0.9 sc/ms only on 'go to goal' missions; 'done'
         // pays the reward stored at mission completion
         double rew = 0.0;
@@ -691,6 +712,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         rs = t0 ? (is_gtg ? rs0 : -1) : (dn ? -1 : rs1);
         term = t0 || dn;
         done = term || trunc;
+        // the episode ends (auto-reset) only on 'forward' into goal / lava, on 'done' or at the time
+        // limit, each of which implies `spec`: the next episode is already in LDS (phase 1e)
+        const bool avail = done && spec;
+        const bool filling = !COMPACT && !done && st.frames < p.n_stack;
         const bool tw = done && (p.terminal_mode == MGX_TERMINAL_ALL ||
                                  (p.terminal_mode == MGX_TERMINAL_TRUNCATED && trunc && !term));
         if (tw && !COMPACT) {                          // stacked terminal_observation: dir + mission
@@ -1281,6 +1306,122 @@ __global__ __launch_bounds__(64) void mgx_scene_kernel(KParams p, int64_t e, uin
     for (int k = 0; k < p.S * p.S; k++) reinterpret_cast<uint8_t *>(rec + 8 + MAX_OBJS)[k] = G.g[k];
 }
 
+// ============================================================== MT ring slider
+// One MT19937 block (624 words) generated in place by a workgroup: the sequential twist
+// (CPython _random.c genrand_uint32) in three data-parallel phases, each read-all -> barrier ->
+// write-all.  new[i] mixes s[i], s[i+1] and x[i] = s[i+397] (i < 227: the old word) or new[i-227]
+// (i >= 227, written by the previous phase); i = 623 takes the new s[0].
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t x) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return x ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+__device__ __forceinline__ void mt_twist_block(uint32_t *s, int tid) {
+    uint32_t v = 0;
+    if (tid < 227) v = mt_mix(s[tid], s[tid + 1], s[tid + 397]);
+    __syncthreads();
+    if (tid < 227) s[tid] = v;
+    __syncthreads();
+    if (tid >= 227 && tid < 454) v = mt_mix(s[tid], s[tid + 1], s[tid - 227]);
+    __syncthreads();
+    if (tid >= 227 && tid < 454) s[tid] = v;
+    __syncthreads();
+    if (tid >= 454 && tid < 624) v = mt_mix(s[tid], s[tid == 623 ? 0 : tid + 1], s[tid - 227]);
+    __syncthreads();
+    if (tid >= 454 && tid < 624) s[tid] = v;
+    __syncthreads();
+}
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    return y ^ (y >> 18);
+}
+
+// Extends the MT ring (MtCtl above).  Pass 1, every workgroup: the minimum live cursor of its
+// SLIDE_ENVS envs -> atomicMin; the last workgroup to finish (fenced counter) runs pass 2: while the
+// ring has room above that minimum, generate whole super-blocks (3,120 words = 312 groups) into the
+// slots of groups no env can read again, at most MT_SLIDE_MAX_SB per launch.  Runs at every refill
+// fork on the refill stream, right before mgx_refill_kernel (and before every inline generation,
+// ring disabled): the launch sequence depends only on the call count (hipGraph-capturable); a
+// launch with nothing to extend costs one 16-KB read pass per 4,096 envs.
+__global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) {
+    __shared__ uint32_t s_st[624];
+    __shared__ uint8_t s_f[MT_SB_WORDS];
+    __shared__ unsigned long long s_red[SLIDE_THREADS / 64];
+    __shared__ unsigned long long s_hi;
+    __shared__ int s_nsb;
+    const int tid = threadIdx.x;
+    MtCtl *c = p.mtc;
+    unsigned long long mn = ~0ull;
+    const int64_t e0 = (int64_t)blockIdx.x * SLIDE_ENVS;
+#pragma unroll
+    for (int k = 0; k < SLIDE_ENVS / SLIDE_THREADS; k++) {
+        const int64_t e = e0 + k * SLIDE_THREADS + tid;
+        if (e < p.n) {
+            const uint4 cr = p.cur_rng[2 * e + 1];
+            unsigned long long v = (unsigned long long)cr.z | ((unsigned long long)cr.w << 32);
+            if (p.start_rng) {
+                const uint4 sr = p.start_rng[2 * e + 1];
+                const unsigned long long u = (unsigned long long)sr.z | ((unsigned long long)sr.w << 32);
+                v = u < v ? u : v;
+            }
+            mn = v < mn ? v : mn;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(mn, off);
+        mn = o < mn ? o : mn;
+    }
+    if ((tid & 63) == 0) s_red[tid >> 6] = mn;
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < SLIDE_THREADS / 64; w++) mn = s_red[w] < mn ? s_red[w] : mn;
+        atomicMin(&c->span_min, mn);
+        __threadfence();
+        s_nsb = atomicAdd(&c->done, 1u) == gridDim.x - 1 ? 1 : -1;   // last workgroup: pass 2
+    }
+    __syncthreads();
+    if (s_nsb < 0) return;
+    if (tid == 0) {
+        __threadfence();
+        const unsigned long long m = atomicExch(&c->span_min, ~0ull);   // every workgroup's minimum; reset
+        c->done = 0;
+        const unsigned long long cap = p.mt_mask + 1, hi = c->hi, need_lo = m / MT_FIELDS;
+        int nsb = 0;
+        while (nsb < MT_SLIDE_MAX_SB && hi + (unsigned long long)(nsb + 1) * MT_SB_GROUPS <= need_lo + cap) nsb++;
+        s_hi = hi;
+        s_nsb = nsb;
+    }
+    __syncthreads();
+    const int nsb = s_nsb;
+    if (nsb == 0) return;
+    for (int i = tid; i < 624; i += SLIDE_THREADS) s_st[i] = c->st[i];
+    __syncthreads();
+    unsigned long long hi = s_hi;
+    for (int sb = 0; sb < nsb; sb++) {
+        for (int b = 0; b < MT_SB_WORDS / 624; b++) {
+            mt_twist_block(s_st, tid);
+            if (tid < 624) s_f[b * 624 + tid] = (uint8_t)(mt_temper(s_st[tid]) >> 27);   // getrandbits(k<=5) field
+        }
+        __syncthreads();
+        if (tid < MT_SB_GROUPS) {
+            uint64_t grp = 0;
+#pragma unroll
+            for (int k = 0; k < MT_FIELDS; k++) grp |= (uint64_t)s_f[tid * MT_FIELDS + k] << (6 * k);
+            const uint64_t slot = (hi + (unsigned long long)tid) & p.mt_mask;
+            p.mt[slot] = grp;
+            if (slot < (uint64_t)MT_PAD) p.mt[p.mt_mask + 1 + slot] = grp;   // mirror: windows stay contiguous
+        }
+        __syncthreads();                                   // s_f is rewritten by the next super-block
+        hi += MT_SB_GROUPS;
+    }
+    for (int i = tid; i < 624; i += SLIDE_THREADS) c->st[i] = s_st[i];
+    if (tid == 0) {
+        c->hi = hi;
+        c->lo = hi > p.mt_mask + 1 ? hi - (p.mt_mask + 1) : 0;
+    }
+}
+
 // ================================================================ GAE kernel
 // DictRolloutBuffer.compute_returns_and_advantage (SB3; fp32, numpy op order,
 // built with -ffp-contract=off):  delta = ((r + (g*nv)*nnt) - V);  last = delta + (c*nnt)*last
@@ -1297,14 +1438,15 @@ __global__ __launch_bounds__(64) void mgx_scene_kernel(KParams p, int64_t e, uin
 constexpr int GAE_TT = 64;                 // steps per tile
 typedef float gf4 __attribute__((ext_vector_type(4)));
 constexpr int GAE_SHARDS = 256;
-__device__ double g_gae_shard[GAE_SHARDS][2];   // (sum A, sum A^2) partials; zero between calls
+static_assert(GAE_SHARDS * 2 == MGX_GAE_SCRATCH_WORDS, "scratch size (include/mgx.h)");
+__device__ double g_gae_shard[GAE_SHARDS][2];   // (sum A, sum A^2) partials when the caller passes no scratch
 
 template <bool DONES>
 __global__ __launch_bounds__(256, 4) void mgx_gae_kernel(const float *__restrict__ r, const float *__restrict__ v,
                                                       const void *__restrict__ es, const float *__restrict__ lv,
                                                       const uint8_t *__restrict__ ld, int64_t T, int64_t N, float g,
                                                       float c, float *__restrict__ adv, float *__restrict__ ret,
-                                                      double *__restrict__ stats) {
+                                                      double *__restrict__ stats, double *__restrict__ shard) {
     __shared__ float s_r[GAE_TT][64], s_v[GAE_TT][64];
     __shared__ uint32_t s_e[GAE_TT][16];                 // flags as bytes (4 columns per dword)
     const int tid = threadIdx.x;
@@ -1401,7 +1543,7 @@ __global__ __launch_bounds__(256, 4) void mgx_gae_kernel(const float *__restrict
             s2 += __shfl_down(s2, off);
         }
         if (tid == 0) {                                   // sharded: 1024 workgroups on 3 addresses would
-            double *sh = g_gae_shard[blockIdx.x & (GAE_SHARDS - 1)];   // serialise at L2 (~40 us)
+            double *sh = shard + 2 * (blockIdx.x & (GAE_SHARDS - 1));   // serialise at L2 (~40 us)
             atomicAdd(&sh[0], s1);
             atomicAdd(&sh[1], s2);
         }
@@ -1410,12 +1552,13 @@ __global__ __launch_bounds__(256, 4) void mgx_gae_kernel(const float *__restrict
 
 // Folds the shards into stats (sum A, sum A^2, count += T*N) and re-zeroes them; runs right after
 // mgx_gae_kernel on the same stream (GAE calls that accumulate stats are stream-ordered).
-__global__ __launch_bounds__(GAE_SHARDS) void mgx_gae_reduce_kernel(double *__restrict__ stats, double count) {
+__global__ __launch_bounds__(GAE_SHARDS) void mgx_gae_reduce_kernel(double *__restrict__ stats, double *__restrict__ shard,
+                                                                      double count) {
     __shared__ double red[2][GAE_SHARDS / 64];
     const int tid = threadIdx.x;
-    double a = g_gae_shard[tid][0], b = g_gae_shard[tid][1];
-    g_gae_shard[tid][0] = 0.0;
-    g_gae_shard[tid][1] = 0.0;
+    double a = shard[2 * tid], b = shard[2 * tid + 1];
+    shard[2 * tid] = 0.0;
+    shard[2 * tid + 1] = 0.0;
     for (int off = 32; off > 0; off >>= 1) {
         a += __shfl_down(a, off);
         b += __shfl_down(b, off);
@@ -1688,7 +1831,7 @@ struct mgx_handle {
                             // (env MGX_REFILL_GENERIC=1: the all-problems kernel, for A/B checks)
     hipStream_t side;       // refill stream
     hipEvent_t ev_fork, ev_done;
-    void *allocs[16];
+    void *allocs[17];
     uint32_t *scene_dev;    // mgx_scene's record (inside allocs[15], inline mode only)
 };
 
@@ -1796,14 +1939,16 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         const char *rg = std::getenv("MGX_REFILL_GENERIC");
         h->refill_multi = !(rg && rg[0] == '1');
     }
+    // MT ring: a power of two of 10-word groups holding at least mt_table_words words (>= 512 groups)
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 24;
-    h->cfg.mt_table_words = (h->cfg.mt_table_words + MT_FIELDS - 1) / MT_FIELDS * MT_FIELDS;
+    int64_t ring_groups = 512;
+    while (ring_groups * MT_FIELDS < h->cfg.mt_table_words && ring_groups < ((int64_t)1 << 26)) ring_groups <<= 1;
+    h->cfg.mt_table_words = ring_groups * MT_FIELDS;
     const int64_t N = cfg->n_envs;
     const int S = cfg->size;
     const int GS = ((S * S) + 15) & ~15;
     const int IMG = FRAME * cfg->n_stack;
-    const int64_t tlen = h->cfg.mt_table_words;
-    const int64_t ngroups = tlen / MT_FIELDS;         // whole groups only (a partial one is never read)
+    const int64_t hi0 = ring_groups * MT_FIELDS / MT_SB_WORDS * MT_SB_GROUPS;   // initial fill: whole super-blocks
 
     auto bail = [&](mgx_status st) {
         for (void *&p : h->allocs) if (p) { (void)hipFree(p); p = nullptr; }
@@ -1812,7 +1957,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         return st;
     };
     size_t sizes[6] = {(size_t)N * sizeof(EnvState), (size_t)N * GS, (size_t)N * 32, (size_t)N * 16,
-                       (size_t)(ngroups + MT_WG + 4) * 8, 256 * 32 + 64};
+                       (size_t)(ring_groups + MT_PAD) * 8, 256 * 32 + 64};
     for (int i = 0; i < 6; i++) {
         hipError_t e = hipMalloc(&h->allocs[i], sizes[i]);
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e)));
@@ -1826,6 +1971,9 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         }
         hipError_t e = hipMemset(h->allocs[11], 0, (size_t)N * 3 + 64);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset ring ctl"));
+        e = hipMemset(h->allocs[10], 0, (size_t)N * 32);      // cursors read by the MT slider before any reset
+        if (e == hipSuccess) e = hipMemset(h->allocs[3], 0, (size_t)N * 16);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset RNG state"));
         e = hipMalloc(&h->allocs[12], (size_t)N * 4 + 64);
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc fix list"));
         e = hipMemset(h->allocs[12], 0, (size_t)N * 4 + 64);
@@ -1837,18 +1985,30 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         e = hipMemset(h->allocs[6], 0, MGX_NCOUNTERS * sizeof(unsigned long long) + 64);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset counters"));
     }
-    // MT19937(base_seed) output stream as packed top-5-bit fields (mgx_device.h: randbelow),
-    // zero-padded by one window
+    // MT19937(base_seed) output stream as packed top-5-bit fields (mgx_device.h: randbelow): the
+    // ring's first hi0 groups + the mirror pad, and the generator state after them (MtCtl), from
+    // which mgx_mt_slide_kernel continues the stream on the device
     {
-        std::vector<uint64_t> tab((size_t)(ngroups + MT_WG + 4), 0ull);
+        std::vector<uint64_t> tab((size_t)(ring_groups + MT_PAD), 0ull);
         HostMT m;
         m.seed((uint64_t)cfg->base_seed);
-        for (int64_t i = 0; i < tlen; i++) {
+        for (int64_t i = 0; i < hi0 * MT_FIELDS; i++) {
             const uint64_t f = m.next() >> 27;
             tab[(size_t)(i / MT_FIELDS)] |= f << (6 * (i % MT_FIELDS));
         }
+        for (int k = 0; k < MT_PAD; k++) tab[(size_t)(ring_groups + k)] = tab[(size_t)k];
         hipError_t e = hipMemcpy(h->allocs[4], tab.data(), tab.size() * 8, hipMemcpyHostToDevice);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "upload MT table"));
+        MtCtl c;
+        std::memset(&c, 0, sizeof c);
+        c.lo = 0;
+        c.hi = (unsigned long long)hi0;
+        c.span_min = ~0ull;
+        std::memcpy(c.st, m.mt, sizeof c.st);         // hi0 * 10 words = whole blocks: m.mti == 624
+        e = hipMalloc(&h->allocs[16], sizeof(MtCtl));
+        if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc MT ring control"));
+        e = hipMemcpy(h->allocs[16], &c, sizeof c, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "upload MT ring control"));
     }
     {
         std::vector<uint8_t> tok(256 * 32 + 64, 0);
@@ -1864,11 +2024,12 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.grid = (uint8_t *)h->allocs[1];
     p.pcg = (uint4 *)h->allocs[2];
     p.aux = (uint4 *)h->allocs[3];
-    p.mt = (const uint64_t *)h->allocs[4];
+    p.mt = (uint64_t *)h->allocs[4];
+    p.mt_mask = (uint64_t)(ring_groups - 1);
+    p.mtc = (MtCtl *)h->allocs[16];
     p.mtok = (const uint8_t *)h->allocs[5];
     p.counters = (unsigned long long *)h->allocs[6];
     p.err = (uint32_t *)((char *)h->allocs[6] + MGX_NCOUNTERS * sizeof(unsigned long long));
-    p.tlen = (uint64_t)ngroups;
     p.n = N;
     p.seed_base = cfg->base_seed + cfg->env_index_offset;
     p.S = S;
@@ -1898,6 +2059,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.n_obstacles = n_obstacles_of(cfg);
     p.vis = cfg->see_through_walls ? 0 : 1;
     p.has_move = (cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL) ? 1 : 0;
+    p.manual = cfg->manual ? 1 : 0;
     p.ring_grid = (uint8_t *)h->allocs[7];
     p.ring_hdr = (uint4 *)h->allocs[8];
     p.ring_rng = (uint4 *)h->allocs[9];
@@ -2007,9 +2169,21 @@ mgx_status mgx_destroy(mgx_handle *h) {
         else hipLaunchKernelGGL((K<4, true>), __VA_ARGS__);                                       \
     } while (0)
 
+// Extends the MT ring ahead of the generator kernels that follow on `stream` (MtCtl).
+static mgx_status launch_slide(mgx_handle *h, void *stream) {
+    const unsigned g = (unsigned)((h->kp.n + SLIDE_ENVS - 1) / SLIDE_ENVS);
+    hipLaunchKernelGGL(mgx_mt_slide_kernel, dim3(g), dim3(SLIDE_THREADS), 0, (hipStream_t)stream, h->kp);
+    HIP_TRY(hipGetLastError());
+    return MGX_OK;
+}
+
 static mgx_status launch_refill(mgx_handle *h, void *stream) {
     if (h->kp.D == 0) return MGX_OK;
     h->refill_launches++;
+    if (!h->kp.initial_fill) {               // (mgx_reset's fill starts where the reset kernel left the cursors)
+        mgx_status ss = launch_slide(h, stream);
+        if (ss != MGX_OK) return ss;
+    }
     const int64_t nblk = (h->kp.n + 63) / 64;
     if (h->refill_multi && !h->ext && h->kp.problem == MGX_PROBLEM_MULTI) {
         const dim3 g((unsigned)nblk), b(64);
@@ -2145,6 +2319,8 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
                            (hipStream_t)stream, h->kp, o, (const int64_t *)actions_dev);
     HIP_TRY(hipGetLastError());
     if (h->kp.D == 0) {   // no ring: every done env is generated inline, right after the step
+        mgx_status ss = launch_slide(h, stream);
+        if (ss != MGX_OK) return ss;
         const unsigned fblk = (unsigned)h->kp.nblk;
         MGX_GEN_LAUNCH(mgx_fixup_kernel, dim3(fblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp, o);
         HIP_TRY(hipGetLastError());
@@ -2246,21 +2422,31 @@ mgx_status mgx_scene(mgx_handle *h, int64_t env, uint32_t *record, void *stream)
     return MGX_OK;
 }
 
+// Per-call shard scratch: the caller's (stats_scratch_dev) or the library's device-global one.
+static double *gae_scratch(double *stats_scratch_dev) {
+    if (stats_scratch_dev) return stats_scratch_dev;
+    void *p = nullptr;
+    (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_gae_shard));
+    return static_cast<double *>(p);
+}
+
 mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const float *episode_starts_dev,
                    const float *last_values_dev, const uint8_t *last_dones_dev, int64_t T, int64_t N, float gamma,
                    float gamma_lambda, float *advantages_dev, float *returns_dev, double *adv_stats_dev,
-                   void *stream) {
+                   double *stats_scratch_dev, void *stream) {
     if (!rewards_dev || !values_dev || !episode_starts_dev || !last_values_dev || !last_dones_dev ||
         !advantages_dev || !returns_dev || T <= 0 || N <= 0)
         return fail(MGX_ERR_INVALID, "mgx_gae: bad argument");
+    double *shard = adv_stats_dev ? gae_scratch(stats_scratch_dev) : nullptr;
+    if (adv_stats_dev && !shard) return fail(MGX_ERR_HIP, "mgx_gae: no shard scratch");
     const int64_t nblk = (N + 63) / 64;
     hipLaunchKernelGGL(mgx_gae_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, rewards_dev,
                        values_dev, (const void *)episode_starts_dev, last_values_dev, last_dones_dev, T, N, gamma,
-                       gamma_lambda, advantages_dev, returns_dev, adv_stats_dev);
+                       gamma_lambda, advantages_dev, returns_dev, adv_stats_dev, shard);
     HIP_TRY(hipGetLastError());
     if (adv_stats_dev) {
         hipLaunchKernelGGL(mgx_gae_reduce_kernel, dim3(1), dim3(GAE_SHARDS), 0, (hipStream_t)stream, adv_stats_dev,
-                           (double)T * (double)N);
+                           shard, (double)T * (double)N);
         HIP_TRY(hipGetLastError());
     }
     return MGX_OK;
@@ -2268,18 +2454,21 @@ mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const floa
 
 mgx_status mgx_gae_dones(const float *rewards_dev, const float *values_dev, const uint8_t *dones_dev,
                          const float *last_values_dev, int64_t T, int64_t N, float gamma, float gamma_lambda,
-                         float *advantages_dev, float *returns_dev, double *adv_stats_dev, void *stream) {
+                         float *advantages_dev, float *returns_dev, double *adv_stats_dev, double *stats_scratch_dev,
+                         void *stream) {
     if (!rewards_dev || !values_dev || !dones_dev || !last_values_dev || !advantages_dev || !returns_dev || T <= 0 ||
         N <= 0)
         return fail(MGX_ERR_INVALID, "mgx_gae_dones: bad argument");
+    double *shard = adv_stats_dev ? gae_scratch(stats_scratch_dev) : nullptr;
+    if (adv_stats_dev && !shard) return fail(MGX_ERR_HIP, "mgx_gae_dones: no shard scratch");
     const int64_t nblk = (N + 63) / 64;
     hipLaunchKernelGGL(mgx_gae_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, rewards_dev,
                        values_dev, (const void *)dones_dev, last_values_dev, (const uint8_t *)nullptr, T, N, gamma,
-                       gamma_lambda, advantages_dev, returns_dev, adv_stats_dev);
+                       gamma_lambda, advantages_dev, returns_dev, adv_stats_dev, shard);
     HIP_TRY(hipGetLastError());
     if (adv_stats_dev) {
         hipLaunchKernelGGL(mgx_gae_reduce_kernel, dim3(1), dim3(GAE_SHARDS), 0, (hipStream_t)stream, adv_stats_dev,
-                           (double)T * (double)N);
+                           shard, (double)T * (double)N);
         HIP_TRY(hipGetLastError());
     }
     return MGX_OK;

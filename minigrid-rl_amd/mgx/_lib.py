@@ -14,10 +14,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MGX_LIB_PATH", os.path.join(HERE, "libmgx.so"))   # override: diagnostic builds
 
 MGX_OK = 0
-ABI_VERSION = 3        # == MGX_ABI_VERSION (include/mgx.h)
+GAE_SCRATCH_WORDS = 512  # == MGX_GAE_SCRATCH_WORDS (include/mgx.h)
+ABI_VERSION = 4        # == MGX_ABI_VERSION (include/mgx.h)
 PROBLEMS = {"multi": 0, "full": 1, "gto": 2, "gtg": 3, "opn": 4, "pkp": 5, "drp": 6, "mov": 7}
 TERMINAL = {"none": 0, "truncated": 1, "all": 2}
-DEVERR = {1: "MT19937 table exhausted", 2: "action outside 0..6 (ValueError: Unknown action)",
+DEVERR = {1: "MT19937 ring: a cursor left the window of the stream the device holds", 2: "action outside 0..6 (ValueError: Unknown action)",
           4: "PCG64 rejection loop bound exceeded", 8: "object list exhausted (AssertionError / IndexError in the reference)",
           16: "episode ring ran dry (engine invariant broken)"}
 
@@ -36,7 +37,7 @@ class MgxConfig(ctypes.Structure):
         ("livelock_words", ctypes.c_int32), ("terminal_mode", ctypes.c_int32),
         ("mission_int64", ctypes.c_int32), ("refill_cap", ctypes.c_int32), ("mt_table_words", ctypes.c_int64),
         ("ring_depth", ctypes.c_int32), ("refill_every", ctypes.c_int32),
-        ("percent_obstacles", ctypes.c_double),
+        ("percent_obstacles", ctypes.c_double), ("manual", ctypes.c_int32), ("reserved0", ctypes.c_int32),
     ]
 
 
@@ -89,8 +90,8 @@ def load():
     L.mgx_join.argtypes = [P, P]
     L.mgx_set_seed.argtypes = [P, I64]
     L.mgx_get_config.argtypes = [P, ctypes.POINTER(MgxConfig)]
-    L.mgx_gae.argtypes = [P, P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P]
-    L.mgx_gae_dones.argtypes = [P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P]
+    L.mgx_gae.argtypes = [P, P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P, P]
+    L.mgx_gae_dones.argtypes = [P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P, P]
     L.mgx_poll_error.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]
     L.mgx_stats.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64)]
     L.mgx_debug_counters.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
@@ -117,3 +118,29 @@ def mission_text(mission_id):
     buf = ctypes.create_string_buffer(64)
     check(load().mgx_mission_text(int(mission_id), buf, 64), "mgx_mission_text")
     return buf.value.decode()
+
+
+# TokenizeVocabWrapper's vocabulary (environment.py:75-81): ' ' '\n' '-' ':' ',' '.' then a..z
+_VOCAB = {c: i for i, c in enumerate(" \n-:,." + "abcdefghijklmnopqrstuvwxyz")}
+
+
+def tokenize(text):
+    """TokenizeVocabWrapper.observation (environment.py:91-112): lower-cased mission text ->
+    32 vocabulary indices, zero-padded."""
+    out = [0] * 32
+    for i, c in enumerate(text.lower()[:32]):
+        out[i] = _VOCAB.get(c, 0)
+    return out
+
+
+def mission_tokens():
+    """u8 [256][32]: the tokens of every mission id (rows of unused ids are zeros) -- what the
+    engine's compact rows carry as one mission-id byte."""
+    import numpy as np
+    tab = np.zeros((256, 32), np.uint8)
+    buf = ctypes.create_string_buffer(64)
+    L = load()
+    for mid in range(256):
+        if L.mgx_mission_text(mid, buf, 64) == MGX_OK:
+            tab[mid] = tokenize(buf.value.decode())
+    return tab

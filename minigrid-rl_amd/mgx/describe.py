@@ -123,6 +123,10 @@ class LLMDescriptionWrapper:
     def __init__(self, engine, problem):
         if engine.ring_depth != 0:
             raise _lib.MgxError("LLMDescriptionWrapper needs MgxEngine(..., ring_depth=-1) (inline resets)")
+        if not getattr(engine, "manual", False):
+            # make_env(manual=True) is the only path that applies this wrapper (environment.py:19-20),
+            # and its PlaygroundEnv ignores a premature 'done' (custom_env.py:325)
+            raise _lib.MgxError("LLMDescriptionWrapper needs MgxEngine(..., manual=True) (make_env(manual=True))")
         self.engine, self.problem = engine, problem
 
     def description(self, env=0):

@@ -25,7 +25,7 @@ class MgxEngine:
                  env_index_offset=0, n_stack=4, all_doors_open=False, see_through_walls=True,
                  obstacles=False, percent_obstacles=0.05, terminal_mode="truncated", mission_dtype=torch.int64,
                  device="cuda", livelock_words=0, mt_table_words=0, reward64=False, ring_depth=0,
-                 refill_every=0, refill_cap=0):
+                 refill_every=0, refill_cap=0, manual=False):
         self.L = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.MgxError("MgxEngine needs a GPU (no CPU fallback by design)")
@@ -59,6 +59,8 @@ class MgxEngine:
         cfg.ring_depth = int(ring_depth)
         cfg.refill_every = int(refill_every)
         cfg.refill_cap = int(refill_cap)
+        cfg.manual = int(bool(manual))
+        self.manual = bool(manual)
         self.terminal_mode = terminal_mode
         self.mission_dtype = torch.int64 if cfg.mission_int64 else torch.uint8
         h = _P()
@@ -204,6 +206,24 @@ class MgxEngine:
             pass
 
 
+_SCRATCH = {}
+
+
+def _stats_scratch(stats):
+    """The adv-stat shard scratch of the calling stream (include/mgx.h, MGX_GAE_SCRATCH_WORDS): GAE calls
+    on different streams (e.g. two collectors) never share partial sums; calls on one stream are ordered."""
+    if stats is None:
+        return None
+    assert stats.dtype == torch.float64 and stats.numel() >= 3 and stats.is_contiguous()
+    stream = torch.cuda.current_stream(stats.device)
+    key = (stats.device.index, stream.cuda_stream)
+    buf = _SCRATCH.get(key)
+    if buf is None:
+        buf = torch.zeros(_lib.GAE_SCRATCH_WORDS, dtype=torch.float64, device=stats.device)
+        _SCRATCH[key] = buf
+    return buf
+
+
 def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lambda, stats=None):
     """DictRolloutBuffer.compute_returns_and_advantage on device (libmgx mgx_gae).
 
@@ -221,8 +241,8 @@ def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lam
     gl = float(torch.tensor(gamma * gae_lambda, dtype=torch.float64).float())   # f32(gamma*lambda in fp64)
     stream = ctypes.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
     _lib.check(L.mgx_gae(_ptr(rewards), _ptr(values), _ptr(episode_starts), _ptr(lv), _ptr(ld), T, N,
-                         ctypes.c_float(gamma), ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats), stream),
-               "mgx_gae")
+                         ctypes.c_float(gamma), ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats),
+                         _ptr(_stats_scratch(stats)), stream), "mgx_gae")
     return adv, ret
 
 
@@ -240,5 +260,6 @@ def gae_dones(rewards, values, dones, last_values, gamma, gae_lambda, stats=None
     gl = float(torch.tensor(gamma * gae_lambda, dtype=torch.float64).float())
     stream = ctypes.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
     _lib.check(L.mgx_gae_dones(_ptr(rewards), _ptr(values), _ptr(dones), _ptr(lv), T, N, ctypes.c_float(gamma),
-                               ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats), stream), "mgx_gae_dones")
+                               ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats), _ptr(_stats_scratch(stats)),
+                               stream), "mgx_gae_dones")
     return adv, ret

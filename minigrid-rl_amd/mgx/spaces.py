@@ -59,11 +59,19 @@ class Dict:
         return "Dict(%s)" % ", ".join("%s: %r" % kv for kv in self.spaces.items())
 
 
-def make_spaces(n_stack, mission_dtype=np.int64):
-    """(observation_space, action_space) of the stacked, transposed env."""
+def make_spaces(n_stack, mission_dtype=np.int64, raw=False):
+    """(observation_space, action_space) of the stacked, transposed env -- or, raw=True, of one
+    wrapped env as make_vec_env hands it out (environment.py:84-89,142): image HWC (7,7,3)."""
     mk_box = (lambda lo, hi, shape, dt: _gs.Box(lo, hi, shape, dt)) if _gs else Box
     mk_dict = _gs.Dict if _gs else Dict
     mk_disc = _gs.Discrete if _gs else Discrete
+    if raw:
+        obs = mk_dict({
+            "direction": mk_box(0, 1, (4,), np.uint8),                 # Discrete2BoxWrapper
+            "image": mk_box(0, 255, (7, 7, 3), np.uint8),              # MiniGridEnv image, [vx][vy][c]
+            "mission": mk_box(0, 32, (32,), mission_dtype),            # TokenizeVocabWrapper
+        })
+        return obs, mk_disc(7)
     obs = mk_dict({
         "direction": mk_box(0, 1, (4 * n_stack,), np.uint8),          # Discrete2BoxWrapper, stacked
         "image": mk_box(0, 255, (3 * n_stack, 7, 7), np.uint8),       # transposed to CHW, stacked

@@ -2,21 +2,38 @@
 
 This is the drop-in for the object the reference builds at src/ppo.py:118-126:
 
-    vec_env = make_vec_env(make_env, n_envs, seed, SubprocVecEnv, env_kwargs=...)
-    vec_env = VecTransposeImage(vec_env)
-    vec_env = VecFrameStack(vec_env, n_frames_stack, channels_order='first')
+    vec_env = make_vec_env(make_env, n_envs, seed, SubprocVecEnv, env_kwargs=...)     # :118-122
+    if cfg.algorithm.n_frames_stack > 1 and not cfg.algorithm.recurrent:               # :124
+        vec_env = VecTransposeImage(vec_env)                                           # :125
+        vec_env = VecFrameStack(vec_env, n_frames_stack, channels_order='first')       # :126
+    model = algo(policy=policy, env=vec_env, **config)                                 # :134-136
 
-It keeps SB3's VecEnv contract (stable_baselines3.common.vec_env.base_vec_env):
+Two modes:
+
+  * raw (`raw=True`, the drop-in for line 118 alone): observations are exactly what
+    make_vec_env's envs return -- image HWC (7,7,3), one-hot direction (4,), mission tokens
+    (32,) int64 (environment.py:84-89,142) -- so lines 124-126 and SB3's own wrappers run
+    unchanged on top, and `PPO(policy, env)` sees the same wrapper chain as in the reference
+    (BaseAlgorithm._wrap_env finds its VecTransposeImage and adds nothing);
+  * fused (default): the engine does VecTransposeImage + VecFrameStack(n, 'first') itself
+    (stacked CHW image (3n,7,7), direction (4n,), mission (32n,)) -- the replacement for
+    lines 118-126 together, for callers that do not pass the env through SB3's _wrap_env
+    (which, not seeing a VecTransposeImage in the chain, would transpose the (3n,7,7) image
+    space again: use raw mode with SB3's algorithms).
+
+When stable_baselines3 is importable the class subclasses its `VecEnv` (so `_wrap_env` does
+not re-wrap it in a DummyVecEnv); otherwise it duck-types the same contract
+(stable_baselines3.common.vec_env.base_vec_env):
 
   * reset() -> obs dict; step_async(actions) / step_wait() -> (obs, rewards
     f32[N], dones bool[N], infos list[N]); step(actions); seed(seed);
     num_envs, observation_space, action_space; close(); get_attr / set_attr /
     env_method / env_is_wrapped for the few attributes the PPO loop reads;
   * obs arrays are COPIES owned by the caller (_obs_from_buf);
-  * infos[i] of a done env carries 'terminal_observation' (the stacked,
-    transposed final obs, VecFrameStack.step_wait), 'TimeLimit.truncated'
-    (truncated and not terminated, SubprocVecEnv worker) and Monitor's
-    'episode' {'r', 'l', 't'}.
+  * infos[i] of a done env carries 'terminal_observation' (the final obs, stacked
+    and transposed in fused mode as VecFrameStack.step_wait does), 'TimeLimit.truncated'
+    (truncated and not terminated, SubprocVecEnv worker) and Monitor's 'episode'
+    {'r', 'l', 't'}.
 
 The PPO loop of this package does not go through here: it keeps everything on
 device (MgxEngine).  This class is for callers that want the reference's host
@@ -30,8 +47,15 @@ import torch
 from .engine import MgxEngine
 from .spaces import make_spaces
 
+try:  # pragma: no cover - SB3 is absent in this image (parity of this layer is unpinned)
+    from stable_baselines3.common.vec_env import VecEnv as _VecEnvBase
+    HAVE_SB3 = True
+except ImportError:  # pragma: no cover
+    _VecEnvBase = object
+    HAVE_SB3 = False
 
-class MgxVecEnv:
+
+class MgxVecEnv(_VecEnvBase):
     """SB3-compatible vectorised PlaygroundEnv on one GPU.
 
     cfg_env mirrors `cfg.env` of the reference (single.yaml: problem, mission,
@@ -41,25 +65,33 @@ class MgxVecEnv:
 
     def __init__(self, n_envs, seed=42, n_frames_stack=4, problem="multi", mission=5, size=8, num_objects=4,
                  all_doors_open=False, see_through_walls=True, obstacles=False, device="cuda",
-                 env_index_offset=0, **engine_kw):
+                 env_index_offset=0, raw=False, **engine_kw):
         self.num_envs = int(n_envs)
-        self.n_stack = int(n_frames_stack)
+        self.raw = bool(raw)
+        self.n_stack = 1 if self.raw else int(n_frames_stack)
         self.engine = MgxEngine(problem=problem, mission=mission, size=size, num_objects=num_objects,
                                 n_envs=n_envs, seed=seed, env_index_offset=env_index_offset, n_stack=self.n_stack,
                                 all_doors_open=all_doors_open, see_through_walls=see_through_walls,
                                 obstacles=obstacles, terminal_mode="all", reward64=True, device=device,
                                 **engine_kw)
-        self.observation_space, self.action_space = make_spaces(self.n_stack)
+        obs_space, act_space = make_spaces(self.n_stack, raw=self.raw)
         self.render_mode = None
-        self._actions = None
-        self._t_start = time.time()
         self._attrs = dict(problem=problem, mission=mission, size=size, num_objects=num_objects,
                            max_steps=size * size, all_doors_open=all_doors_open,
-                           see_through_walls=see_through_walls)
+                           see_through_walls=see_through_walls, render_mode=None)
+        if HAVE_SB3:
+            _VecEnvBase.__init__(self, self.num_envs, obs_space, act_space)
+        else:
+            self.observation_space, self.action_space = obs_space, act_space
+            self.reset_infos = [{} for _ in range(self.num_envs)]
+        self._seeds = [None] * self.num_envs
+        self._actions = None
+        self._t_start = time.time()
         dev = self.engine.device
         self._act_dev = torch.zeros(self.num_envs, dtype=torch.int64, device=dev)
         pin = torch.cuda.is_available()
-        self._host = {k: torch.empty(v.shape, dtype=v.dtype, pin_memory=pin) for k, v in self.engine.obs.items()}
+        self._host = {k: torch.empty(self._host_shape(k, v), dtype=v.dtype, pin_memory=pin)
+                      for k, v in self.engine.obs.items()}
         self._host_scalars = torch.empty((4, self.num_envs), dtype=torch.float64, pin_memory=pin)
         self._ep_start = np.full(self.num_envs, time.time())
 
@@ -69,10 +101,12 @@ class MgxVecEnv:
         if seed is None:
             seed = int(np.random.randint(0, 2 ** 31 - 1))
         self.engine.set_seed(seed)
-        return [seed + i for i in range(self.num_envs)]
+        self._seeds = [seed + i for i in range(self.num_envs)]
+        return list(self._seeds)
 
     def reset(self):
         self.engine.reset()
+        self._seeds = [None] * self.num_envs
         self._ep_start[:] = time.time()
         return self._obs_to_host(self.engine.obs)
 
@@ -103,7 +137,7 @@ class MgxVecEnv:
         idx = np.nonzero(dones)[0]
         if idx.size:
             sel = torch.as_tensor(idx, device=e.device)
-            t_obs = {k: v.index_select(0, sel).cpu().numpy() for k, v in e.terminal_obs.items()}
+            t_obs = {k: self._layout(k, v.index_select(0, sel)).cpu().numpy() for k, v in e.terminal_obs.items()}
             now = time.time()
             for j, i in enumerate(idx):
                 infos[i]["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
@@ -122,7 +156,7 @@ class MgxVecEnv:
         self.engine.close()
 
     def render(self, mode=None):
-        raise NotImplementedError("rendering is outside the engine's scope (DESIGN.md §8)")
+        raise NotImplementedError("rendering is outside the engine's scope (DESIGN.md §9)")
 
     def get_attr(self, attr_name, indices=None):
         if attr_name not in self._attrs:
@@ -142,7 +176,7 @@ class MgxVecEnv:
                 for _ in self._indices(indices)]
 
     def get_images(self):
-        raise NotImplementedError("rendering is outside the engine's scope (DESIGN.md §8)")
+        raise NotImplementedError("rendering is outside the engine's scope (DESIGN.md §9)")
 
     @property
     def unwrapped(self):
@@ -156,8 +190,19 @@ class MgxVecEnv:
             return [indices]
         return indices
 
+    def _host_shape(self, key, v):
+        if self.raw and key == "image":          # (N, 3, 7, 7) [c][vx][vy] -> the env's (N, 7, 7, 3)
+            return (v.shape[0], 7, 7, 3)
+        return tuple(v.shape)
+
+    def _layout(self, key, v):
+        """Engine tensor -> the layout this VecEnv hands out (raw mode: the env's HWC image)."""
+        if self.raw and key == "image":
+            return v.permute(0, 2, 3, 1)
+        return v
+
     def _obs_to_host(self, obs):
         for k, v in obs.items():
-            self._host[k].copy_(v, non_blocking=True)
+            self._host[k].copy_(self._layout(k, v), non_blocking=True)
         torch.cuda.current_stream(self.engine.device).synchronize()
         return {k: v.numpy().copy() for k, v in self._host.items()}

@@ -262,6 +262,7 @@ typedef struct {
     jmp_buf jb;
     objrec_t objs[MAXOBJ]; int nobjs;
     int range_x[MAXS * 2], range_y[MAXS * 2], nrange;   /* self.target_range */
+    int manual;     /* PlaygroundEnv(manual=True) (custom_env.py:325): 'done' ends only a completed mission */
 } env_t;
 
 typedef struct {
@@ -921,9 +922,11 @@ static void env_step(env_t *e, int action, uint8_t img[7][7][3], double *rew, in
             *rew = r; *term = 1; *trunc = truncated;
             return;
         }
-        e->mission_done = 0; e->has_reward = 0;   /* not manual */
-        *rew = 0.0; *term = 1; *trunc = truncated;
-        return;
+        if (!e->manual) {                          /* elif not self.manual (custom_env.py:325-328) */
+            e->mission_done = 0; e->has_reward = 0;
+            *rew = 0.0; *term = 1; *trunc = truncated;
+            return;
+        }
     }
     *rew = reward; *term = terminated; *trunc = truncated;
 }
@@ -954,6 +957,9 @@ EXPORT orc_vec *orc_create(int problem, int mission, int size, int num_objects, 
 }
 
 EXPORT void orc_destroy(orc_vec *v) { if (v) { free(v->e); free(v); } }
+
+/* PlaygroundEnv(manual=...) of every env (make_env(manual=True), environment.py:10-20). */
+EXPORT void orc_set_manual(orc_vec *v, int manual) { for (int i = 0; i < v->n; i++) v->e[i].manual = manual; }
 
 static void emit_obs(env_t *e, int i, uint8_t *img_src, uint8_t *img, uint8_t *dir, uint8_t *mis) {
     if (img) memcpy(img + (size_t)i * 147, img_src, 147);

@@ -45,6 +45,7 @@ def lib():
         L.orc_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                                       ctypes.c_int, ctypes.c_int, ctypes.c_double]
         L.orc_destroy.argtypes = [P]
+        L.orc_set_manual.argtypes = [P, ctypes.c_int]
         L.orc_reset.argtypes = [P, ctypes.c_int64, ctypes.c_int64, P, P, P, P]
         L.orc_reset_ex.argtypes = [P, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, P, P, P, P]
         L.orc_step.argtypes = [P] * 12
@@ -70,7 +71,7 @@ class OracleVec:
     def __init__(self, problem="multi", mission=5, size=8, num_objects=4, n_envs=16,
                  seed=42, index_offset=0, all_doors_open=False,
                  livelock_words=LIVELOCK_WORDS, see_through_walls=True, obstacles=False,
-                 percent_obstacles=0.05):
+                 percent_obstacles=0.05, manual=False):
         self.L = lib()
         self.n, self.S, self.seed, self.offset = n_envs, size, seed, index_offset
         m = -1 if mission is None else int(mission)
@@ -79,6 +80,8 @@ class OracleVec:
                                    int(obstacles), float(percent_obstacles))
         if not self.h:
             raise ValueError("orc_create failed")
+        if manual:
+            self.L.orc_set_manual(self.h, 1)
 
     def close(self):
         if self.h:

@@ -98,7 +98,7 @@ def pcg_state(env):
 class RefVec:
     """N reference envs with SubprocVecEnv-style private MT streams."""
 
-    def __init__(self, cfg, n):
+    def __init__(self, cfg, n, manual=False):
         self.ce, self.envm = load_reference()
         self.cfg = cfg
         self.n = n
@@ -108,7 +108,15 @@ class RefVec:
             rng = CountingRandom(cfg.seed)
             self.rngs.append(rng)
             with self._bind(i):
-                self.envs.append(self.envm.make_env("custom", None, cfg=cfg, manual=False))
+                if manual:
+                    # PlaygroundEnv(manual=True) -- make_env(manual=True)'s env (environment.py:12); the
+                    # observation wrappers of the training path (TokenizeVocab + Discrete2Box, :22,29)
+                    # instead of LLMDescriptionWrapper, so the fixture has the usual layout
+                    env = self.ce.PlaygroundEnv(render_mode=None, cfg=cfg, manual=True)
+                    env = self.envm.Discrete2BoxWrapper(self.envm.TokenizeVocabWrapper(env))
+                    self.envs.append(env)
+                else:
+                    self.envs.append(self.envm.make_env("custom", None, cfg=cfg, manual=False))
 
     class _Bind:
         def __init__(self, outer, i):
@@ -162,9 +170,9 @@ def target_info(env):
     return tx, ty, ta
 
 
-def run_config(name, cfg, n, T, seed_actions=1234):
+def run_config(name, cfg, n, T, seed_actions=1234, manual=False):
     S = cfg.env.size
-    vec = RefVec(cfg, n)
+    vec = RefVec(cfg, n, manual=manual)
     acts = np.random.default_rng(seed_actions).integers(0, 7, (T, n)).astype(np.int8)
     d = {}
 
@@ -251,7 +259,7 @@ def run_config(name, cfg, n, T, seed_actions=1234):
                           cfg.env.num_objects], np.int64)
     d["problem"] = np.array(cfg.env.problem)
     d["env_flags"] = np.array([int(bool(cfg.env.see_through_walls)), int(bool(cfg.env.obstacles)),
-                               int(bool(cfg.env.all_doors_open))], np.int64)
+                               int(bool(cfg.env.all_doors_open)), int(bool(manual))], np.int64)
     d["percent_obstacles"] = np.array(float(cfg.env.percent_obstacles), np.float64)
     names = sorted(missions)
     d["mission_names"] = np.array(names)
@@ -289,6 +297,11 @@ CONFIGS += [
     ("ado_multi_tgl_s16", dict(problem="multi", mission=1, size=16, all_doors_open=True)),
     ("ado_multi_gtg_s8", dict(problem="multi", mission=5, size=8, all_doors_open=True)),
     ("ado_single_opn_s8", dict(problem="opn", mission=None, size=8, all_doors_open=True)),
+    # manual=True (make_env(manual=True), the LLMDescriptionWrapper / GUI path): a premature 'done'
+    # is a no-op (custom_env.py:319-328), so episodes end only on goal / lava / completed missions /
+    # the time limit
+    ("manual_multi_all_s8", dict(problem="multi", mission=None, size=8, manual=True)),
+    ("manual_multi_pkp_s11", dict(problem="multi", mission=2, size=11, manual=True)),
 ]
 
 
@@ -304,8 +317,10 @@ def main():
         if args.only and args.only not in name:
             continue
         t0 = time.time()
+        kw = dict(kw)
+        manual = kw.pop("manual", False)
         cfg = make_cfg(**kw)
-        d = run_config(name, cfg, args.n, args.T)
+        d = run_config(name, cfg, args.n, args.T, manual=manual)
         np.savez_compressed(os.path.join(out_dir, name + ".npz"), **d)
         print("%-22s %6.1fs resets=%d livelocks=%d" % (
             name, time.time() - t0, int((d["terminated"] | d["truncated"]).sum()),

@@ -17,7 +17,8 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-CASES = [dict(problem="multi", mission=None, size=8, n=200, n_stack=4),
+CASES = [dict(problem="multi", mission=5, size=8, n=4000, n_stack=4),      # BASELINE config 2's GTG
+         dict(problem="multi", mission=None, size=8, n=200, n_stack=4),
          dict(problem="multi", mission=1, size=16, n=130, n_stack=4, see_through_walls=False),
          dict(problem="multi", mission=2, size=11, n=77, n_stack=3, all_doors_open=True),
          dict(problem="pkp", mission=None, size=8, n=64, n_stack=1)]

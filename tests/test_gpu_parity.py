@@ -62,6 +62,65 @@ class EngineSource:
         return self.e.dump_state()
 
 
+class CompactSource:
+    """libmgx's COMPACT layout -- mgx_step_compact, the kernel bench.py times -- behind
+    trajcheck's compare() protocol.  Each step writes one 148-B observation row (byte 0
+    direction, bytes 1..147 the [c][vx][vy] frame) + a mission-id byte into a CompactBuffer of
+    T rows (carried over when full, as the collector does); where an episode ended the buffer
+    row is the new episode's first observation and the terminal row (terminal_mode 'all') the
+    finished one's final frame, whose mission id is the previous row's (include/mgx.h)."""
+
+    def __init__(self, cfg, T=64, ring_depth=0, refill_every=0, terminal_mode="all", n_stack=4):
+        from mgx import MgxEngine
+        from mgx._lib import mission_tokens
+        from mgx.compact import CompactBuffer
+        kw = dict(cfg)
+        self.n = kw.pop("n_envs")
+        self.e = MgxEngine(n_envs=self.n, n_stack=n_stack, terminal_mode=terminal_mode, reward64=True,
+                           mission_dtype=torch.uint8, ring_depth=ring_depth, refill_every=refill_every, **kw)
+        self.buf = CompactBuffer(self.e, T)
+        self.tok = torch.as_tensor(mission_tokens(), device=self.e.device)
+        self.t = 0
+
+    @staticmethod
+    def decode(rows):
+        """u8 [n, 148] device rows -> (image HWC [n, 7, 7, 3], direction [n]) on the host."""
+        img = rows[:, 1:].reshape(-1, 3, 7, 7).permute(0, 2, 3, 1).contiguous().cpu().numpy()
+        return img, rows[:, 0].cpu().numpy()
+
+    def tokens(self, mids):
+        return self.tok[mids.long()].cpu().numpy()
+
+    def reset(self):
+        self.e.reset()
+        self.buf.observe(0)
+        self.t = 0
+        r = self.buf.row(0)
+        img, d = self.decode(self.buf.rows[r])
+        return dict(image=img, dir=d, mission=self.tokens(self.buf.mids[r]), livelock=self.e.livelock.cpu().numpy())
+
+    def step(self, a):
+        if self.t == self.buf.T:
+            self.buf.carry_over()
+            self.t = 0
+        t = self.t
+        self.buf.step(t, torch.as_tensor(np.ascontiguousarray(a), device=self.e.device))
+        self.t += 1
+        r = self.buf.row(t + 1)
+        dd = self.buf.starts[r].cpu().numpy().astype(bool)
+        img, d = self.decode(self.buf.rows[r])
+        timg, td = self.decode(self.buf.terminal_rows)
+        m, tm = self.tokens(self.buf.mids[r]), self.tokens(self.buf.mids[r - 1])
+        return dict(image=np.where(dd[:, None, None, None], timg, img), dir=np.where(dd, td, d),
+                    mission=np.where(dd[:, None], tm, m), reward=self.e.reward64.cpu().numpy(),
+                    terminated=self.buf.terminated[t].cpu().numpy(), truncated=self.buf.truncated[t].cpu().numpy(),
+                    r_image=img, r_dir=d, r_mission=m, livelock=self.e.livelock.cpu().numpy(),
+                    reward32=self.buf.rewards[t].cpu().numpy())
+
+    def dump(self):
+        return self.e.dump_state()
+
+
 FIXTURES = TC.fixtures()
 
 
@@ -79,12 +138,16 @@ def test_unsatisfiable_or_invalid_configs_are_rejected(kw):
         MgxEngine(n_envs=64, **kw)
 
 
+@pytest.mark.parametrize("layout", ["sb3", "compact"])
 @pytest.mark.parametrize("path", FIXTURES, ids=lambda p: p.split("/")[-1][:-4])
-def test_engine_matches_reference_fixture(path):
+def test_engine_matches_reference_fixture(path, layout):
+    """Every reference fixture (every step, every state field, every RNG position) through both
+    observation layouts: the SB3 stacks (mgx_step, the VecEnv drop-in) and the compact rows
+    (mgx_step_compact, the kernel the headline bench times)."""
     _need_gpu()
     d = dict(np.load(path))
     cfg, T = TC.fixture_cfg(d)
-    src = EngineSource(cfg)
+    src = EngineSource(cfg) if layout == "sb3" else CompactSource(cfg)
     msg = TC.compare(src, d)
     src.e.poll_error()
     assert msg is None, msg
@@ -93,14 +156,20 @@ def test_engine_matches_reference_fixture(path):
 @pytest.mark.parametrize("name", ["multi_all_s8", "multi_gtg_s8", "multi_tgl_s16", "single_pkp_s8",
                                   "single_full_s8", "obst_single_mov_s11", "novis_obst_multi_tgl_s16",
                                   "ado_multi_all_s11"])
-@pytest.mark.parametrize("ring", [(-1, 0), (2, 1), (4, 2), (8, 3)], ids=["inline", "ring2", "ring4", "ring8_every3"])
+@pytest.mark.parametrize("ring", [(-1, 0, "sb3"), (2, 1, "sb3"), (4, 2, "sb3"), (8, 3, "sb3"), (2, 1, "compact"),
+                                  (8, 3, "compact")],
+                         ids=["inline", "ring2", "ring4", "ring8_every3", "compact_ring2", "compact_ring8_every3"])
 def test_engine_reset_paths_match_fixture(name, ring):
     """Same fixtures through the other reset paths: episodes generated inline in
-    the step kernel (no ring) and small rings refilled at different cadences."""
+    the step kernel (no ring) and small rings refilled at different cadences (the compact
+    layout needs the ring)."""
     _need_gpu()
     d = dict(np.load(TC.GOLDEN + "/traj/%s.npz" % name))
     cfg, T = TC.fixture_cfg(d)
-    src = EngineSource(cfg, ring_depth=ring[0], refill_every=ring[1])
+    if ring[2] == "sb3":
+        src = EngineSource(cfg, ring_depth=ring[0], refill_every=ring[1])
+    else:
+        src = CompactSource(cfg, T=37, ring_depth=ring[0], refill_every=ring[1])
     msg = TC.compare(src, d)
     src.e.poll_error()
     assert msg is None, msg
@@ -277,34 +346,137 @@ FULL_SIZE = [("multi", 5, 8, 65536, 64),       # BASELINE config 2 (1 GPU)
              ("multi", 1, 16, 131072, 24)]     # config 5, one GPU's shard of 1,048,576
 
 
+@pytest.mark.parametrize("layout", ["sb3", "compact"])
 @pytest.mark.parametrize("problem,mission,size,n,T", FULL_SIZE, ids=["cfg2_65536", "cfg4_32768", "cfg5_131072"])
-def test_full_size_matches_oracle(problem, mission, size, n, T):
-    """Every env at the BASELINE per-GPU sizes against the C oracle: per step the done flags,
-    the f64 rewards and the newest raw frame of all n envs; after T steps every env's full
-    state (grid, agent, carrying, step count, mission flags, stored reward, MT cursor, PCG64
-    state, target)."""
+def test_full_size_matches_oracle(problem, mission, size, n, T, layout):
+    """Every env at the BASELINE per-GPU sizes against the C oracle, in both observation layouts
+    (compact = the kernel the headline bench times): per step the done flags, the f64 and f32
+    rewards, the terminated / truncated flags, the final frame of every env (the terminal frame
+    where done), the new episode's first frame and mission where done; after T steps every env's
+    full state (grid, agent, carrying, step count, mission flags, stored reward, MT cursor,
+    PCG64 state, target)."""
     _need_gpu()
     import oracle as O
-    from mgx import MgxEngine
     ov = O.OracleVec(problem, mission, size, 4, n, 42)
-    eng = MgxEngine(problem=problem, mission=mission, size=size, n_envs=n, n_stack=4, terminal_mode="all",
-                    reward64=True)
+    cfg = dict(problem=problem, mission=mission, size=size, n_envs=n)
+    src = EngineSource(cfg) if layout == "sb3" else CompactSource(cfg, T=T)
     r = ov.reset()
-    obs = eng.reset()
-    img, _, mi = EngineSource.newest(obs)
-    assert np.array_equal(img, r["image"]) and np.array_equal(mi, r["mission"])
+    g = src.reset()
+    assert np.array_equal(g["image"], r["image"]) and np.array_equal(g["mission"], r["mission"])
+    assert np.array_equal(g["dir"], r["dir"])
     acts = np.random.default_rng(2024).integers(0, 7, (T, n)).astype(np.int32)
-    acts_dev = torch.as_tensor(acts, device=eng.device)
     for t in range(T):
         o = ov.step(acts[t])
-        obs = eng.step(acts_dev[t])
-        done = eng.done.cpu().numpy().astype(bool)
-        assert np.array_equal(done, (o["terminated"] | o["truncated"]).astype(bool)), t
-        assert np.array_equal(eng.reward64.cpu().numpy(), o["reward"]), t
-        img = obs["image"][:, -3:].permute(0, 2, 3, 1).cpu().numpy()
-        timg = eng.terminal_obs["image"][:, -3:].permute(0, 2, 3, 1).cpu().numpy()
-        assert np.array_equal(np.where(done[:, None, None, None], timg, img), o["image"]), t
-        assert np.array_equal(img[done], o["r_image"][done]), t
+        s = src.step(acts[t])
+        done = (o["terminated"] | o["truncated"]).astype(bool)
+        for k in ("terminated", "truncated", "reward", "image", "dir", "mission"):
+            assert np.array_equal(np.asarray(s[k]).astype(o[k].dtype), o[k]), (t, k)
+        if layout == "compact":
+            assert np.array_equal(s["reward32"], o["reward"].astype(np.float32)), t
+        for k in ("r_image", "r_dir", "r_mission"):
+            assert np.array_equal(s[k][done], o[k][done]), (t, k)
+    eng = src.e
+    a, b = eng.dump_state(), ov.dump()
+    for k in ("grid", "agent", "carrying", "step_count", "mission_done", "mtwords", "pcg", "target"):
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a["stored_reward"], b["stored_reward"], equal_nan=True)
+    eng.poll_error()
+
+
+@pytest.mark.parametrize("n", [8192, 65536])
+def test_bench_shape_graph_matches_oracle(n):
+    """The exact shape bench.py times (its default and the driver's 20-step line): GTG 8x8,
+    compact layout, terminal_mode 'truncated', refill epoch E = 20 = horizon H, one hipGraph per
+    chunk holding the carry-over, 20 mgx_step_compact launches (the first forks the epoch's
+    refill), mgx_gae_dones with the adv-stat triple and mgx_join -- replayed 4 times with new
+    actions in its static buffer.  Every replay: each step's observation rows, mission ids, dones,
+    terminated / truncated flags and f32 rewards vs the C oracle, the terminal row of every env
+    that was truncated, GAE advantages / returns bit-exact vs numpy and the (sum A, sum A^2, n)
+    triple; at the end every env's state."""
+    _need_gpu()
+    import oracle as O
+    from mgx import MgxEngine, gae_dones
+    from mgx._lib import mission_tokens
+    from mgx.compact import CompactBuffer
+    E, W, reps = 20, 200, 4                       # W: eager warm-up steps (10 refill epochs)
+    ov = O.OracleVec("multi", 5, 8, 4, n, 42)
+    eng = MgxEngine(problem="multi", mission=5, size=8, n_envs=n, n_stack=4, terminal_mode="truncated",
+                    refill_every=E)
+    assert eng.refill_every == E
+    dev = eng.device
+    buf = CompactBuffer(eng, E)
+    H = buf.H
+    tok = mission_tokens()
+    rng = np.random.default_rng(77)
+    acts = rng.integers(0, 7, (W + reps * E, n)).astype(np.int32)
+    ov.reset()
+    eng.reset()
+    buf.observe(0)
+    for t in range(W):
+        if t and t % E == 0:
+            buf.carry_over()
+        buf.step(t % E, torch.as_tensor(acts[t], device=dev))
+        ov.step(acts[t])
+    eng.join()
+    torch.cuda.synchronize()
+    vals = torch.as_tensor(rng.standard_normal((E, n)).astype(np.float32), device=dev)
+    last_v = torch.as_tensor(rng.standard_normal(n).astype(np.float32), device=dev)
+    adv, ret = torch.empty((E, n), device=dev), torch.empty((E, n), device=dev)
+    st = torch.zeros(3, dtype=torch.float64, device=dev)
+    static = torch.zeros((E, n), dtype=torch.int32, device=dev)
+    gamma, lam = 0.8108071290665859, 0.9452281119742252
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        gr = torch.cuda.CUDAGraph()
+        gr.capture_begin()
+        st.zero_()
+        buf.carry_over()
+        for j in range(E):
+            buf.step(j, static[j])
+        gae_dones(buf.rewards, vals, buf.dones, last_v, gamma, lam, stats=st, out=(adv, ret))
+        eng.join()
+        gr.capture_end()
+    torch.cuda.synchronize()
+    for r in range(reps):
+        static.copy_(torch.as_tensor(acts[W + r * E:W + (r + 1) * E], device=dev))
+        gr.replay()
+        torch.cuda.synchronize()
+        rows = buf.rows.cpu().numpy()
+        mids = buf.mids.cpu().numpy()
+        starts = buf.starts.cpu().numpy().astype(bool)
+        rew = buf.rewards.cpu().numpy()
+        trm, trc = buf.terminated.cpu().numpy(), buf.truncated.cpu().numpy()
+        t_img = np.zeros((n, 7, 7, 3), np.uint8)
+        t_has = np.zeros(n, bool)
+        for j in range(E):
+            o = ov.step(acts[W + r * E + j])
+            done = (o["terminated"] | o["truncated"]).astype(bool)
+            row = rows[H + 1 + j]
+            img = row[:, 1:].reshape(n, 3, 7, 7).transpose(0, 2, 3, 1)
+            want_img = np.where(done[:, None, None, None], o["r_image"], o["image"])
+            assert np.array_equal(img, want_img), (r, j, "image")
+            assert np.array_equal(row[:, 0], np.where(done, o["r_dir"], o["dir"])), (r, j, "dir")
+            assert np.array_equal(tok[mids[H + 1 + j]], np.where(done[:, None], o["r_mission"], o["mission"])), (r, j)
+            assert np.array_equal(starts[H + 1 + j], done), (r, j, "done")
+            assert np.array_equal(trm[j], o["terminated"]) and np.array_equal(trc[j], o["truncated"]), (r, j)
+            assert np.array_equal(rew[j], o["reward"].astype(np.float32)), (r, j, "reward")
+            tr = o["truncated"].astype(bool) & ~o["terminated"].astype(bool)
+            t_img[tr] = o["image"][tr]
+            t_has |= tr
+        assert t_has.any()
+        trows = buf.terminal_rows.cpu().numpy()
+        got_t = trows[:, 1:].reshape(n, 3, 7, 7).transpose(0, 2, 3, 1)
+        assert np.array_equal(got_t[t_has], t_img[t_has]), (r, "terminal rows")
+        dn = starts[H + 1:H + 1 + E]
+        es = np.zeros((E, n), np.float32)
+        es[1:] = dn[:-1]
+        want_a, want_r = O.gae(rew, vals.cpu().numpy(), es, last_v.cpu().numpy(), dn[-1], gamma, lam)
+        assert np.array_equal(adv.cpu().numpy(), want_a), r
+        assert np.array_equal(ret.cpu().numpy(), want_r), r
+        sv = st.cpu().numpy()
+        w = want_a.astype(np.float64)
+        assert sv[2] == E * n and abs(sv[0] - w.sum()) <= 1e-9 * np.abs(w).sum() + 1e-9, (r, sv)
+        assert abs(sv[1] - (w * w).sum()) <= 1e-9 * (w * w).sum(), (r, sv)
     a, b = eng.dump_state(), ov.dump()
     for k in ("grid", "agent", "carrying", "step_count", "mission_done", "mtwords", "pcg", "target"):
         assert np.array_equal(a[k], b[k]), k
@@ -407,3 +579,89 @@ def test_ring_never_runs_dry_under_max_consumption(ring):
     a_, b_ = eng.dump_state(), ov.dump()
     for k in ("grid", "agent", "mtwords", "pcg"):
         assert np.array_equal(a_[k], b_[k]), k
+
+
+@pytest.mark.parametrize("ring_depth", [0, -1], ids=["ring", "inline"])
+def test_mt_stream_outlives_its_ring(ring_depth):
+    """The shared MT19937(42) stream (custom_env.py:82, one CPython `random` per env) never runs
+    out: the device ring of MT output is a fraction of what the envs consume here (mt_table_words
+    = 2^16 -> 8,192 groups = 81,920 words), and mgx_mt_slide_kernel keeps generating the stream on
+    the device ahead of the live cursors.  GTG 8x8, 1,024 envs stepped until the furthest cursor
+    has passed several ring lengths, with an unseeded VecEnv.reset() in the middle (both streams
+    continue from each env's current episode, so its cursor must still be in the ring):
+    transitions bit-exact vs the C oracle (per-env CPython MT state), every RNG position equal at
+    the end, and no MGX_DEVERR_MT_TABLE."""
+    _need_gpu()
+    import oracle as O
+    from mgx import MgxEngine
+    n = 1024
+    T = 36000 if ring_depth == 0 else 24000
+    ov = O.OracleVec("multi", 5, 8, 4, n, 42)
+    eng = MgxEngine(problem="multi", mission=5, size=8, n_envs=n, n_stack=4, terminal_mode="none", reward64=True,
+                    mt_table_words=1 << 16, ring_depth=ring_depth)
+    ring_words = 8192 * 10
+    ov.reset()
+    eng.reset()
+    rng = np.random.default_rng(31)
+    acts = torch.as_tensor(rng.integers(0, 7, (T, n)).astype(np.int32), device=eng.device)
+    acts_h = acts.cpu().numpy()
+    for t in range(T):
+        if t == T // 2:
+            r = ov.reset(seed=None)
+            obs = eng.reset()
+            img, dr, mi = EngineSource.newest(obs)
+            assert np.array_equal(img, r["image"]) and np.array_equal(mi, r["mission"]), "reset at %d" % t
+        o = ov.step(acts_h[t])
+        obs = eng.step(acts[t])
+        if t % 50 == 0 or t == T - 1:
+            done = eng.done.cpu().numpy().astype(bool)
+            assert np.array_equal(done, (o["terminated"] | o["truncated"]).astype(bool)), t
+            assert np.array_equal(eng.reward64.cpu().numpy(), o["reward"]), t
+            img, _, mi = EngineSource.newest(obs)
+            assert np.array_equal(img, np.where(done[:, None, None, None], o["r_image"], o["image"])), t
+    eng.poll_error()                         # raises on MGX_DEVERR_MT_TABLE
+    a, b = eng.dump_state(), ov.dump()
+    for k in ("grid", "agent", "carrying", "step_count", "mission_done", "mtwords", "pcg", "target"):
+        assert np.array_equal(a[k], b[k]), k
+    assert a["mtwords"].min() > 2 * ring_words, a["mtwords"].min()     # every env went round the ring > 2x
+
+
+def test_gae_stats_of_overlapping_streams_stay_apart():
+    """Two GAE calls with advantage statistics in flight at once on two streams (two collectors):
+    each stream's partial sums go through its own shard scratch (include/mgx.h,
+    MGX_GAE_SCRATCH_WORDS), so each triple is its own rollout's."""
+    _need_gpu()
+    import oracle as O
+    from mgx import gae_dones
+    dev = torch.device("cuda")
+    g, lam = 0.8108071290665859, 0.9452281119742252
+    rng = np.random.default_rng(41)
+    T, N = 256, 65536
+    data = []
+    for k in range(2):
+        r = rng.standard_normal((T, N)).astype(np.float32) * (1 + 3 * k)
+        v = rng.standard_normal((T, N)).astype(np.float32)
+        d = (rng.random((T, N)) < 0.15).astype(np.uint8)
+        lv = rng.standard_normal(N).astype(np.float32)
+        data.append((r, v, d, lv))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    dev_data = [tuple(torch.as_tensor(x, device=dev) for x in dd) for dd in data]
+    stats = [torch.zeros(3, dtype=torch.float64, device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    outs = []
+    for rep in range(3):
+        for k in range(2):
+            with torch.cuda.stream(streams[k]):
+                r, v, d, lv = dev_data[k]
+                outs.append(gae_dones(r, v, d, lv, g, lam, stats=stats[k]))
+    torch.cuda.synchronize()
+    for k in range(2):
+        r, v, d, lv = data[k]
+        es = np.zeros((T, N), np.float32)
+        es[1:] = d[:-1]
+        want_a, _ = O.gae(r, v, es, lv, d[-1], g, lam)
+        w = want_a.astype(np.float64)
+        s = stats[k].cpu().numpy()
+        assert s[2] == 3 * T * N, s
+        assert abs(s[0] - 3 * w.sum()) <= 1e-9 * 3 * np.abs(w).sum() + 1e-9, (k, s)
+        assert abs(s[1] - 3 * (w * w).sum()) <= 1e-9 * 3 * (w * w).sum(), (k, s)

@@ -12,7 +12,18 @@ FIXTURES = TC.fixtures()
 
 
 def test_fixtures_present():
-    assert len(FIXTURES) == 37
+    assert len(FIXTURES) == 39
+
+
+def test_manual_fixtures_hold_premature_dones():
+    """The manual=True fixtures (PlaygroundEnv(manual=True), custom_env.py:319-328) contain 'done'
+    actions that end nothing (mission not complete) and 'done' actions that end a completed
+    mission with its stored reward."""
+    for name in ("manual_multi_all_s8", "manual_multi_pkp_s11"):
+        d = dict(np.load(TC.GOLDEN + "/traj/%s.npz" % name))
+        a, term = d["actions"], d["terminated"]
+        assert ((a == 6) & (term == 0)).sum() > 100, name
+        assert ((a == 6) & (term == 1) & (d["reward"] > 0)).sum() > 0, name
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=lambda p: p.split("/")[-1][:-4])

@@ -94,3 +94,68 @@ def test_vec_env_matches_sb3_stack(problem, mission, size, n_stack):
     for k in ("grid", "agent", "mission_done", "mtwords", "pcg"):
         assert np.array_equal(a[k], b[k]), k
     env.close()
+
+
+class TransposeStack:
+    """src/ppo.py:125-126 restated over a raw VecEnv: VecTransposeImage (image HWC -> CHW, the
+    infos' terminal_observation too), then VecFrameStack(n_stack, 'first') (roll, zero done
+    envs' stacks, re-stack terminal_observation) -- SB3 2.x semantics, unpinned."""
+
+    def __init__(self, venv, n_stack):
+        import oracle as O
+        self.O, self.venv = O, venv
+        self.fs = O.FrameStackOracle(venv.num_envs, n_stack)
+        self.num_envs = venv.num_envs
+
+    def _t(self, obs):
+        return dict(image=self.O.vec_transpose_image(obs["image"]), direction=obs["direction"],
+                    mission=obs["mission"].astype(np.int64))
+
+    def reset(self):
+        return self.fs.reset(self._t(self.venv.reset()))
+
+    def step(self, a):
+        o, r, d, infos = self.venv.step(a)
+        cur = self._t(o)
+        term_frames = {k: np.zeros_like(v) for k, v in cur.items()}
+        for i in np.nonzero(d)[0]:
+            t = self._t({k: np.asarray(v)[None] for k, v in infos[i]["terminal_observation"].items()})
+            for k in t:
+                term_frames[k][i] = t[k][0]
+        obs, term = self.fs.step(cur, d, term_frames)
+        for i in np.nonzero(d)[0]:
+            infos[i] = dict(infos[i])
+            infos[i]["terminal_observation"] = {k: v[i] for k, v in term.items()}
+        return obs, r, d, infos
+
+
+@pytest.mark.parametrize("problem,mission,size,n_stack", [("multi", 5, 8, 4), ("multi", None, 11, 2)])
+def test_raw_mode_under_sb3_wrappers_matches_reference_stack(problem, mission, size, n_stack):
+    """MgxVecEnv(raw=True) -- the drop-in for make_vec_env alone (ppo.py:118-122) -- hands out the
+    wrapped env's own observation (image HWC (7,7,3), one-hot direction, int64 tokens) and raw
+    terminal observations, so the reference's unchanged lines 124-126 stack it: that chain must
+    equal the SubprocVecEnv + VecTransposeImage + VecFrameStack restatement over the C oracle in
+    every obs, reward, done and info."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mgx import MgxVecEnv
+    n, T = 192, 160
+    kw = dict(problem=problem, mission=mission, size=size, num_objects=4, seed=42)
+    ref = OracleVecEnv(n, n_stack, **kw)
+    raw = MgxVecEnv(n, raw=True, **kw)
+    sp = raw.observation_space
+    assert sp["image"].shape == (7, 7, 3) and sp["direction"].shape == (4,) and sp["mission"].shape == (32,)
+    env = TransposeStack(raw, n_stack)
+    assert _same_obs(env.reset(), ref.reset())
+    rng = np.random.default_rng(23)
+    for t in range(T):
+        a = rng.integers(0, 7, n)
+        o1, r1, d1, i1 = env.step(a)
+        o2, r2, d2, i2 = ref.step(a.astype(np.int32))
+        assert _same_obs(o1, o2), t
+        assert np.array_equal(r1, r2) and np.array_equal(d1, d2), t
+        for i in np.nonzero(d2)[0]:
+            assert i1[i]["TimeLimit.truncated"] == i2[i]["TimeLimit.truncated"], (t, i)
+            assert _same_obs(i1[i]["terminal_observation"], i2[i]["terminal_observation"]), (t, i)
+            assert i1[i]["episode"]["l"] == i2[i]["episode"]["l"], (t, i)
+    raw.close()

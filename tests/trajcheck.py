@@ -25,10 +25,14 @@ def fixture_cfg(d):
     flags = [int(x) for x in d["env_flags"]] if "env_flags" in d else [1, 0]
     stw, obst = flags[0], flags[1]
     ado = flags[2] if len(flags) > 2 else 0          # all_doors_open (third flag, added in round 2)
+    manual = flags[3] if len(flags) > 3 else 0       # PlaygroundEnv(manual=True) (fourth flag, round 3)
     pct = float(d["percent_obstacles"]) if "percent_obstacles" in d else 0.05
-    return dict(problem=str(d["problem"]), mission=None if mission < 0 else mission, size=S,
-                num_objects=nobj, n_envs=n, seed=seed, see_through_walls=bool(stw), obstacles=bool(obst),
-                percent_obstacles=pct, all_doors_open=bool(ado)), T
+    cfg = dict(problem=str(d["problem"]), mission=None if mission < 0 else mission, size=S,
+               num_objects=nobj, n_envs=n, seed=seed, see_through_walls=bool(stw), obstacles=bool(obst),
+               percent_obstacles=pct, all_doors_open=bool(ado))
+    if manual:
+        cfg["manual"] = True
+    return cfg, T
 
 
 def _eq(a, b):
@@ -98,7 +102,7 @@ class OracleSource:
                              cfg["seed"], see_through_walls=cfg.get("see_through_walls", True),
                              obstacles=cfg.get("obstacles", False),
                              percent_obstacles=cfg.get("percent_obstacles", 0.05),
-                             all_doors_open=cfg.get("all_doors_open", False))
+                             all_doors_open=cfg.get("all_doors_open", False), manual=cfg.get("manual", False))
 
     def reset(self):
         return self.v.reset()
