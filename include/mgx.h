@@ -252,7 +252,8 @@ mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits);
  * queued in the rings now (between two mgx_reset calls, episodes produced by
  * the refill = resets consumed + change of [4]), [5] refill launches enqueued (incl. the
  * synchronous fills of mgx_reset), [6] mgx_step calls since the last mgx_reset,
- * [7] reserved (0).  Synchronises `stream` and the refill stream. */
+ * [7] MT19937 words generated so far (the device ring holds the last mt_table_words of them).
+ * Synchronises `stream` and the refill stream. */
 mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]);
 
 /* Diagnostics: the first n (<= 32) raw device counters (phase / section clocks of

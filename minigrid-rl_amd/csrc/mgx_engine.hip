@@ -52,19 +52,27 @@ constexpr int FROW = 148;                  // LDS frame row (fast roll): byte 0 
 // the generator's state after them (a whole number of 624-word blocks).  No env ever reads below
 // its oldest live cursor again -- the end of its current episode (cur_rng: a later VecEnv.reset()
 // continues from there) or, in inline mode, that episode's start (start_rng: mgx_scene regenerates
-// it) -- so mgx_mt_slide_kernel extends the stream on the device to that minimum plus the ring's
-// size, overwriting dead groups: the stream never runs out (round 2's host-built table of 2^24
-// words lasted ~1.1-1.5 M steps per env).
+// it) -- so mgx_mt_slide_kernel keeps the stream generated MT_AHEAD words past the furthest
+// producer cursor, overwriting only dead groups (at most the ring's size above the oldest live
+// cursor): the stream never runs out (round 2's host-built table of 2^24 words lasted ~1.1-1.5 M
+// steps per env).  What the ring bounds is the SPREAD of the live cursors: every env reads the same
+// stream at its own pace, and per-episode consumption is heavy-tailed (an abandoned live-locked
+// attempt takes 4,096 words), so the spread grows like sqrt(steps) -- measured at GTG 8x8, 1,024
+// envs: 74 k words after 4,900 steps.  The default ring (2^26 words) holds that spread for ~10^9
+// steps per env at 65,536 envs; past it MGX_DEVERR_MT_TABLE is raised, never silent.
 struct MtCtl {
     unsigned long long lo, hi;       // groups of the stream held by the ring
     unsigned long long span_min;     // min live cursor (words) of the running slide pass, ~0 between passes
+    unsigned long long span_max;     // max producer cursor (words) of the running pass, 0 between passes
     unsigned int done;               // workgroups of the running pass that have reduced
     unsigned int pad;
     uint32_t st[624];                // MT19937 state at word hi * 10 (every output of it consumed)
 };
 constexpr int MT_SB_WORDS = 3120;                         // lcm(624, 10): five MT blocks = 312 whole groups
 constexpr int MT_SB_GROUPS = MT_SB_WORDS / MT_FIELDS;
-constexpr int MT_SLIDE_MAX_SB = 8;                        // super-blocks one slide generates at most (25 k words)
+constexpr int MT_SLIDE_MAX_SB = 64;                       // super-blocks one slide generates at most (200 k words)
+constexpr unsigned long long MT_AHEAD = 1ull << 19;       // words kept generated past the furthest producer cursor
+constexpr long long MT_HOST_FILL = 1ll << 20;             // words the host generates at create
 constexpr int SLIDE_THREADS = 1024, SLIDE_ENVS = 4 * SLIDE_THREADS;
 // LDS bytes per resetting lane: MT window + objs list (obj_stride words, see mgx_create)
 __host__ __device__ constexpr int scratch_per_env(int obj_stride) { return WIN_STRIDE * 4 + obj_stride * 4; }
@@ -1347,12 +1355,12 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
 __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) {
     __shared__ uint32_t s_st[624];
     __shared__ uint8_t s_f[MT_SB_WORDS];
-    __shared__ unsigned long long s_red[SLIDE_THREADS / 64];
+    __shared__ unsigned long long s_red[SLIDE_THREADS / 64], s_red2[SLIDE_THREADS / 64];
     __shared__ unsigned long long s_hi;
     __shared__ int s_nsb;
     const int tid = threadIdx.x;
     MtCtl *c = p.mtc;
-    unsigned long long mn = ~0ull;
+    unsigned long long mn = ~0ull, mx = 0;
     const int64_t e0 = (int64_t)blockIdx.x * SLIDE_ENVS;
 #pragma unroll
     for (int k = 0; k < SLIDE_ENVS / SLIDE_THREADS; k++) {
@@ -1366,17 +1374,25 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
                 v = u < v ? u : v;
             }
             mn = v < mn ? v : mn;
+            const uint4 ax = p.aux[e];                        // producer cursor (mgx_refill_kernel)
+            const unsigned long long w = (unsigned long long)ax.z | ((unsigned long long)ax.w << 32);
+            mx = w > mx ? w : mx;
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(mn, off);
+        const unsigned long long o = __shfl_xor(mn, off), q = __shfl_xor(mx, off);
         mn = o < mn ? o : mn;
+        mx = q > mx ? q : mx;
     }
-    if ((tid & 63) == 0) s_red[tid >> 6] = mn;
+    if ((tid & 63) == 0) { s_red[tid >> 6] = mn; s_red2[tid >> 6] = mx; }
     __syncthreads();
     if (tid == 0) {
-        for (int w = 1; w < SLIDE_THREADS / 64; w++) mn = s_red[w] < mn ? s_red[w] : mn;
+        for (int w = 1; w < SLIDE_THREADS / 64; w++) {
+            mn = s_red[w] < mn ? s_red[w] : mn;
+            mx = s_red2[w] > mx ? s_red2[w] : mx;
+        }
         atomicMin(&c->span_min, mn);
+        atomicMax(&c->span_max, mx);
         __threadfence();
         s_nsb = atomicAdd(&c->done, 1u) == gridDim.x - 1 ? 1 : -1;   // last workgroup: pass 2
     }
@@ -1384,11 +1400,15 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     if (s_nsb < 0) return;
     if (tid == 0) {
         __threadfence();
-        const unsigned long long m = atomicExch(&c->span_min, ~0ull);   // every workgroup's minimum; reset
+        const unsigned long long m = atomicExch(&c->span_min, ~0ull);   // every workgroup's extremes; reset
+        const unsigned long long x = atomicExch(&c->span_max, 0ull);
         c->done = 0;
         const unsigned long long cap = p.mt_mask + 1, hi = c->hi, need_lo = m / MT_FIELDS;
-        int nsb = 0;
-        while (nsb < MT_SLIDE_MAX_SB && hi + (unsigned long long)(nsb + 1) * MT_SB_GROUPS <= need_lo + cap) nsb++;
+        const unsigned long long want_hi = (x + MT_AHEAD) / MT_FIELDS;    // generated this far ahead ...
+        int nsb = 0;                                                      // ... within the ring above need_lo
+        while (nsb < MT_SLIDE_MAX_SB && hi + (unsigned long long)nsb * MT_SB_GROUPS < want_hi &&
+               hi + (unsigned long long)(nsb + 1) * MT_SB_GROUPS <= need_lo + cap)
+            nsb++;
         s_hi = hi;
         s_nsb = nsb;
     }
@@ -1940,7 +1960,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         h->refill_multi = !(rg && rg[0] == '1');
     }
     // MT ring: a power of two of 10-word groups holding at least mt_table_words words (>= 512 groups)
-    if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 24;
+    if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 26;
     int64_t ring_groups = 512;
     while (ring_groups * MT_FIELDS < h->cfg.mt_table_words && ring_groups < ((int64_t)1 << 26)) ring_groups <<= 1;
     h->cfg.mt_table_words = ring_groups * MT_FIELDS;
@@ -1948,7 +1968,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     const int S = cfg->size;
     const int GS = ((S * S) + 15) & ~15;
     const int IMG = FRAME * cfg->n_stack;
-    const int64_t hi0 = ring_groups * MT_FIELDS / MT_SB_WORDS * MT_SB_GROUPS;   // initial fill: whole super-blocks
+    // initial fill: whole super-blocks, MT_HOST_FILL words at most (the slider generates the rest)
+    const int64_t hi0 = std::min(ring_groups * MT_FIELDS, (int64_t)MT_HOST_FILL) / MT_SB_WORDS * MT_SB_GROUPS;
 
     auto bail = [&](mgx_status st) {
         for (void *&p : h->allocs) if (p) { (void)hipFree(p); p = nullptr; }
@@ -1989,21 +2010,23 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     // ring's first hi0 groups + the mirror pad, and the generator state after them (MtCtl), from
     // which mgx_mt_slide_kernel continues the stream on the device
     {
-        std::vector<uint64_t> tab((size_t)(ring_groups + MT_PAD), 0ull);
+        std::vector<uint64_t> tab((size_t)hi0, 0ull);            // slots [hi0, ring) are written before read
         HostMT m;
         m.seed((uint64_t)cfg->base_seed);
         for (int64_t i = 0; i < hi0 * MT_FIELDS; i++) {
             const uint64_t f = m.next() >> 27;
             tab[(size_t)(i / MT_FIELDS)] |= f << (6 * (i % MT_FIELDS));
         }
-        for (int k = 0; k < MT_PAD; k++) tab[(size_t)(ring_groups + k)] = tab[(size_t)k];
         hipError_t e = hipMemcpy(h->allocs[4], tab.data(), tab.size() * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess)                                       // mirror pad = slots 0 .. MT_PAD-1
+            e = hipMemcpy((uint64_t *)h->allocs[4] + ring_groups, tab.data(), (size_t)MT_PAD * 8, hipMemcpyHostToDevice);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "upload MT table"));
         MtCtl c;
         std::memset(&c, 0, sizeof c);
         c.lo = 0;
         c.hi = (unsigned long long)hi0;
         c.span_min = ~0ull;
+        c.span_max = 0;
         std::memcpy(c.st, m.mt, sizeof c.st);         // hi0 * 10 words = whole blocks: m.mti == 624
         e = hipMalloc(&h->allocs[16], sizeof(MtCtl));
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc MT ring control"));
@@ -2500,6 +2523,11 @@ mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]) {
     }
     c[5] = h->refill_launches;
     c[6] = h->calls;
+    {
+        MtCtl m;
+        HIP_TRY(hipMemcpy(&m, h->kp.mtc, 16, hipMemcpyDeviceToHost));   // lo, hi
+        c[7] = m.hi * (uint64_t)MT_FIELDS;
+    }
     for (int i = 0; i < 8; i++) out[i] = c[i];
     return MGX_OK;
 }

@@ -172,7 +172,7 @@ class MgxEngine:
         out = (ctypes.c_uint64 * 8)()
         _lib.check(self.L.mgx_stats(self.h, self._stream(), out), "mgx_stats")
         return dict(steps=int(out[0]), resets=int(out[1]), livelocks=int(out[2]), max_mt_cursor=int(out[3]),
-                    queued=int(out[4]), refill_launches=int(out[5]), calls=int(out[6]))
+                    queued=int(out[4]), refill_launches=int(out[5]), calls=int(out[6]), mt_generated=int(out[7]))
 
     def debug_counters(self, n=32):
         """Raw diagnostic counters (section clocks of the stamp builds)."""

@@ -1,0 +1,95 @@
+"""BASELINE config 3 learning evidence: PPO (mgx.ppo.learn: the reference's PPO(CustomPPOPolicy,
+vec_env).learn restated over the engine) on PKP 8x8, then the success rate over 1,000 deterministic
+evaluation episodes on a fresh engine (README.md:54-65 "Benchmark (1k ep)": success = the episode
+paid a reward, i.e. the mission was completed; the reference reports PKP 57%).
+
+The reference trains 16 envs x horizon 1024 with minibatch 256 (algorithm/ppo.yaml); at 65,536 envs
+the same update count per sample would take 16,384 optimiser steps per 16-step rollout, so this run
+keeps the reference's ratio of optimiser steps per rollout (4 epochs x 64 minibatches) with larger
+minibatches -- stated in the output, a knob that changes optimisation (SURVEY.md §7 hard part 5).
+
+  python tools/ppo_learn.py [--timesteps 1e8] [--n-envs 65536] [--horizon 16] [--batch-size 16384]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "minigrid-rl_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def success_rate(policy, env_kw, n_episodes, seed, deterministic=True):
+    from mgx import MgxEngine, evaluate_policy
+    eng = MgxEngine(n_envs=n_episodes, seed=seed, n_stack=4, terminal_mode="none", reward64=True,
+                    mission_dtype=torch.uint8, **env_kw)
+    if policy is None:                                  # uniform random actions (reference point)
+        g = torch.Generator(device=eng.device)
+        g.manual_seed(seed)
+        act = lambda obs: torch.randint(0, 7, (eng.n,), device=eng.device, generator=g)   # noqa: E731
+        rews, lens = evaluate_policy(act, eng, n_episodes, return_episode_rewards=True)
+    else:
+        policy.train(False)
+        rews, lens = evaluate_policy(policy, eng, n_episodes, deterministic=deterministic, return_episode_rewards=True)
+    eng.close()
+    r = np.asarray(rews)
+    return dict(episodes=int(r.size), success_rate=float((r > 0).mean()), mean_reward=float(r.mean()),
+                mean_length=float(np.mean(lens)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--timesteps", type=float, default=1e8)
+    ap.add_argument("--n-envs", type=int, default=65536)
+    ap.add_argument("--horizon", type=int, default=16)
+    ap.add_argument("--batch-size", type=int, default=16384)
+    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--lr0", type=float, default=1e-3)        # README.md:19-51 first-stage schedule (pkp0)
+    ap.add_argument("--lr1", type=float, default=3e-5)
+    ap.add_argument("--mission", type=int, default=2)
+    ap.add_argument("--size", type=int, default=8)
+    ap.add_argument("--eval-episodes", type=int, default=1000)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    from mgx.ppo import PPOConfig, learn
+    env_kw = dict(problem="multi", mission=args.mission, size=args.size, num_objects=4)
+    cfg = PPOConfig(n_envs=args.n_envs, horizon=args.horizon, batch_size=args.batch_size, n_epochs=args.epochs,
+                    initial_learning_rate=args.lr0, final_learning_rate=args.lr1, env=env_kw)
+    t0 = time.perf_counter()
+    curve = []
+
+    def log(st):
+        if "timesteps" in st:
+            curve.append({k: st[k] for k in ("timesteps", "ep_rew_mean", "ep_len_mean", "lr", "kl", "clipfrac")})
+            if len(curve) % 10 == 1:
+                print("t=%.0fs %s" % (time.perf_counter() - t0, json.dumps(curve[-1])), file=sys.stderr, flush=True)
+    random_eval = success_rate(None, env_kw, args.eval_episodes, seed=4242)
+    pol, hist, eng = learn(cfg, int(args.timesteps), log=log)
+    train_s = time.perf_counter() - t0
+    eng.close()
+    ev = success_rate(pol, env_kw, args.eval_episodes, seed=4242)
+    out = {"what": "PPO (mgx.ppo.learn) on %s, then evaluate_policy over %d deterministic episodes on a fresh "
+                   "engine (seed 4242)" % ("PKP" if args.mission == 2 else "mission %d" % args.mission,
+                                           args.eval_episodes),
+           "config": {"env": env_kw, "n_envs": cfg.n_envs, "horizon": cfg.horizon, "batch_size": cfg.batch_size,
+                      "n_epochs": cfg.n_epochs, "optimizer_steps_per_rollout": cfg.n_epochs * cfg.n_envs *
+                      cfg.horizon // cfg.batch_size, "lr": [cfg.initial_learning_rate, cfg.final_learning_rate],
+                      "other_hyperparameters": "algorithm/ppo.yaml (gamma, gae_lambda, clip ranges, ent/vf coef, "
+                                               "max_grad_norm)"},
+           "timesteps": hist[-1]["timesteps"] if hist else 0, "rollouts": len(hist), "train_seconds": train_s,
+           "env_steps_per_s_incl_training": (hist[-1]["timesteps"] / train_s) if hist else None,
+           "eval": ev, "eval_random_policy": random_eval,
+           "reference": "README.md:61 PPO PKP model on PKP: 57% (1k episodes; size and training steps unstated)",
+           "curve": curve[::max(1, len(curve) // 40)]}
+    print(json.dumps(out))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
