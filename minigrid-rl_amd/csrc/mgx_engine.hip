@@ -508,7 +508,6 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     __shared__ uint8_t s_dlist[BLOCK_ENVS];      // envs that popped a new episode (render + mission lists)
     __shared__ uint8_t s_flist[BLOCK_ENVS];      // envs whose mission stack is still filling
     __shared__ uint8_t s_fslot[BLOCK_ENVS];      // ... and the slot that flips 0 -> tokens
-    __shared__ uint32_t s_rp2[BLOCK_ENVS];       // render params of the popped episodes' first frames
     __shared__ uint8_t s_popf[BLOCK_ENVS];       // env popped a new episode (its grid is in s_pgrid)
     __shared__ int s_nd, s_npop, s_nf;
     __shared__ unsigned long long s_dmask, s_tmask;   // done / terminal-written envs as bit masks
@@ -606,40 +605,46 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         for (int c = tid >> 6; c < (p.GS >> 4); c += BLOCK_THREADS / 64)
             __builtin_amdgcn_global_load_lds(src + c, s_grid + c * (BLOCK_ENVS * 16), 16, 0, 0);
     }
-    // (e) wave 0: SubprocVecEnv auto-reset, speculatively.  A step can end the episode only
-    // on 'forward' (goal / lava ahead), on 'done' or at the time limit, which the state and
-    // the action alone tell; for those envs the next pre-generated episode (header, tokens,
-    // grid, RNG snapshot) is fetched now, in a second round trip of this phase, and used only
-    // if the step does end it.  Envs whose stack is still filling fetch their mission's tokens.
-    bool spec = false;
-    if (tid < ne) {
-        if (!COMPACT && st.frames < p.n_stack) {
-            const uint4 *t = reinterpret_cast<const uint4 *>(p.mtok + st.mission_id * 32);
-            __builtin_amdgcn_global_load_lds(t, s_tokA, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(t + 1, s_tokB, 16, 0, 0);
-        }
-        spec = p.D > 0 && (a == A_FORWARD || a == A_DONE || st.step_count + 1 >= S * S) &&
-               (uint8_t)(rpub - rhead) != 0;
-        if (spec) {
-            const int64_t slot = (e0 + tid) * p.D + (rhead & (p.D - 1));
-            __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot, s_phdr, 16, 0, 0);
-            if (!COMPACT) {
-                __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 1, s_ptokA, 16, 0, 0);
-                __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 2, s_ptokB, 16, 0, 0);
-            }
-            __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot, s_prng, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot + 1, s_prng + BLOCK_ENVS, 16, 0, 0);
-            const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
-            for (int c = 0; c < (p.GS >> 4); c++)
-                __builtin_amdgcn_global_load_lds(gsrc + c, s_pgrid + c * (BLOCK_ENVS * 16), 16, 0, 0);
-        }
-        // (no register load here: its phi copy after the branch would wait on the DMA above)
-    }
+    // (e) SubprocVecEnv auto-reset, speculatively.  A step can end the episode only on
+    // 'forward' (goal / lava ahead), on 'done' or at the time limit, which the state and the
+    // action alone tell (every wave holds them for env tid mod 64); for those envs the next
+    // pre-generated episode (header, tokens, grid, RNG snapshot) is fetched, and used only if
+    // the step does end it.  Envs whose stack is still filling fetch their mission's tokens.
+    // This second round trip depends on the first, so WAVE 1 issues it and goes on to the
+    // barrier without waiting: its latency runs under wave 0's step logic, and only the pop
+    // (after the post-logic barrier, which wave 1 reaches once the DMA has landed) reads it.
+    const bool spec = p.D > 0 && (a == A_FORWARD || a == A_DONE || st.step_count + 1 >= S * S) &&
+                      (uint8_t)(rpub - rhead) != 0;
+    const bool wave1 = (tid >> 6) == 1;
     // Every phase-1 load of this wave has landed (register loads and LDS-DMA alike).  Saying
     // so explicitly matters: otherwise the waitcnt pass assumes a qa/qb load may be pending
     // on some path and puts a vmcnt(0) before every roll quad of phase 3, which then waits
     // on the previous quad's STORES (vmcnt counts both) and serialises the whole roll.
     __builtin_amdgcn_s_waitcnt(0);
+    if (wave1) {
+        const int lw = tid - BLOCK_ENVS;
+        if (lw < ne) {
+            if (!COMPACT && st.frames < p.n_stack) {
+                const uint4 *t = reinterpret_cast<const uint4 *>(p.mtok + st.mission_id * 32);
+                __builtin_amdgcn_global_load_lds(t, s_tokA, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(t + 1, s_tokB, 16, 0, 0);
+            }
+            if (spec) {
+                const int64_t slot = (e0 + lw) * p.D + (rhead & (p.D - 1));
+                __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot, s_phdr, 16, 0, 0);
+                if (!COMPACT) {
+                    __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 1, s_ptokA, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 2, s_ptokB, 16, 0, 0);
+                }
+                __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot, s_prng, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot + 1, s_prng + BLOCK_ENVS, 16, 0, 0);
+                const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
+                for (int c = 0; c < (p.GS >> 4); c++)
+                    __builtin_amdgcn_global_load_lds(gsrc + c, s_pgrid + c * (BLOCK_ENVS * 16), 16, 0, 0);
+            }
+            // (no register load here: its phi copy after the branch would wait on the DMA above)
+        }
+    }
     __syncthreads();
 #ifdef MGX_STAMPS
     ts1 = __builtin_amdgcn_s_memtime();
@@ -738,28 +743,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             // puts a vmcnt(0) (which waits on every STORE in flight) before the mission writer
             __builtin_amdgcn_s_waitcnt(0);
         }
-        if (avail) {
-            const uint4 h = s_phdr[tid];
-            p.cur_rng[2 * e] = s_prng[tid];
-            p.cur_rng[2 * e + 1] = s_prng[BLOCK_ENVS + tid];
-            if (p.has_move) p.range_cur[e] = p.ring_range[e * p.D + (rhead & (p.D - 1))];
+        if (avail) {                                 // the pop itself follows the next barrier
             new_head = (int)(uint8_t)(rhead + 1);   // published after a barrier, loads consumed
-            const int nax = h.x & 0xFF, nay = (h.x >> 8) & 0xFF, ndir = (h.x >> 16) & 0xFF;
-            const uint8_t mid = (uint8_t)(h.y >> 16);
-            EnvState ns;
-            ns.ax = (uint8_t)nax; ns.ay = (uint8_t)nay; ns.dir = (uint8_t)ndir; ns.carry = 0;
-            ns.step_count = 0; ns.reward_step = (int16_t)rs;          // survives the reset (Q2)
-            ns.tx = (uint8_t)(h.x >> 24); ns.ty = (uint8_t)h.y; ns.target_action = (uint8_t)(h.y >> 8);
-            ns.mission_id = mid;
-            ns.mission_done = (uint8_t)mdone; ns.frames = 1; ns.flags = 0; ns.pad = 0;
-            p.state[e] = ns;
-            s_rp2[tid] = (uint32_t)nax | ((uint32_t)nay << 8) | ((uint32_t)ndir << 16);
-            if (COMPACT) static_cast<uint8_t *>(o.mis)[e] = mid;
-            else dir_stack_fresh(o.dir, e, p.n_stack, ndir);
-            if (o.livelock) o.livelock[e] = (int)h.z;
             dirty = true;
             popped = true;
-            if (h.z) atomicAdd(&s_ll, (unsigned long long)h.z);
         } else if (done && p.D > 0) {
             my_err |= MGX_DEVERR_RING_EMPTY;   // cannot happen (refill production rule)
         } else if (done) {
@@ -813,7 +800,30 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         }
     }
     if (my_err) atomicOr(p.err, my_err);
+    if (wave1) __builtin_amdgcn_s_waitcnt(0);          // the auto-reset prefetch has landed in LDS
     __syncthreads();
+    // SubprocVecEnv auto-reset: the env takes the popped episode (its header and RNG snapshot
+    // were prefetched by wave 1 under the step logic).
+    if (popped) {
+        const int64_t e = e0 + tid;
+        const uint4 h = s_phdr[tid];
+        p.cur_rng[2 * e] = s_prng[tid];
+        p.cur_rng[2 * e + 1] = s_prng[BLOCK_ENVS + tid];
+        if (p.has_move) p.range_cur[e] = p.ring_range[e * p.D + (rhead & (p.D - 1))];
+        const int ndir = (h.x >> 16) & 0xFF;
+        const uint8_t mid = (uint8_t)(h.y >> 16);
+        EnvState ns;
+        ns.ax = (uint8_t)(h.x & 0xFF); ns.ay = (uint8_t)((h.x >> 8) & 0xFF); ns.dir = (uint8_t)ndir; ns.carry = 0;
+        ns.step_count = 0; ns.reward_step = (int16_t)rs;          // survives the reset (Q2)
+        ns.tx = (uint8_t)(h.x >> 24); ns.ty = (uint8_t)h.y; ns.target_action = (uint8_t)(h.y >> 8);
+        ns.mission_id = mid;
+        ns.mission_done = (uint8_t)mdone; ns.frames = 1; ns.flags = 0; ns.pad = 0;
+        p.state[e] = ns;
+        if (COMPACT) static_cast<uint8_t *>(o.mis)[e] = mid;
+        else dir_stack_fresh(o.dir, e, p.n_stack, ndir);
+        if (o.livelock) o.livelock[e] = (int)h.z;
+        if (h.z) atomicAdd(&s_ll, (unsigned long long)h.z);
+    }
     // ring heads: the popped slot is consumed (its DMA landed in phase 1), so the refill may
     // reuse it.  Every lane writes its head, changed or not: one 64-B store per block instead
     // of a byte store per popped env.
@@ -904,7 +914,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         const int le = tid >> 2, q = tid & 3;
         if (le < ne) {
             const bool pop = s_popf[le];
-            const uint32_t rp = pop ? s_rp2[le] : s_rp[le];
+            const uint32_t rp = pop ? (s_phdr[le].x & 0xFFFFFFu) : s_rp[le];   // popped: ax | ay<<8 | dir<<16
             render_cols(pop ? s_pgrid : s_grid, S, le, q, rp, s_stk + le * FSTRIDE + FOFF);
             if (COMPACT && q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);   // row byte 0: direction
         }
