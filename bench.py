@@ -55,6 +55,7 @@ PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_STEP = 334                    # per env-step algorithmic bytes
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
 PMC_FILE_COMPACT = os.path.join(ROOT, "profiles", "pmc_step_kernel_compact.json")
+PMC_FILE_FUSED = os.path.join(ROOT, "profiles", "pmc_rollout_kernel.json")
 
 
 def parse():
@@ -83,9 +84,11 @@ def parse():
     ap.add_argument("--batch-size", type=int, default=65536, help="ppo: minibatch size")
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
     ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layout")
-    ap.add_argument("--layout", default=None, choices=["compact", "sb3"],
-                    help="observation storage: compact rows + mgx_gather (mgx_step_compact; the default of "
-                         "both workloads) or the materialised SB3 stacks (mgx_step, the VecEnv drop-in's)")
+    ap.add_argument("--layout", default=None, choices=["compact", "sb3", "fused"],
+                    help="observation storage: compact rows + mgx_gather (mgx_step_compact, one launch per "
+                         "step; the default of both workloads), the same rows from one launch per refill epoch "
+                         "(fused: mgx_rollout_compact, actions known up front) or the materialised SB3 stacks "
+                         "(mgx_step, the VecEnv drop-in's)")
     args = ap.parse_args()
     presets = {2: dict(mission="5", size=8, n_envs=65536), 4: dict(mission="None", size=8, n_envs=32768),
                5: dict(mission="1", size=16, n_envs=131072)}
@@ -376,7 +379,9 @@ def measure_rollout(args, layout, world, rank, dev):
     # rollout storage the steps write directly (compact layout): reward f32 and done u8 per step;
     # values are synthetic (the rollout bench has no policy); GAE + the (sum A, sum A^2, n)
     # all-reduce run once per horizon inside the timed region
-    compact = layout == "compact"
+    fused = layout == "fused"
+    compact = layout in ("compact", "fused")
+    assert not fused or (aligned and H % E == 0), "fused rollouts need whole refill epochs"
     cbuf = None
     if compact:
         # compact layout: each step writes its observation row, reward and done straight into the
@@ -396,10 +401,13 @@ def measure_rollout(args, layout, world, rank, dev):
     stream = torch.cuda.current_stream(dev)
     if compact:
         cbuf.observe(0)
-        for t in range(W):
+        for t in range(0, W, E if fused else 1):
             if t and t % H == 0:
                 cbuf.carry_over()
-            cbuf.step(t % H, actions[t])
+            if fused:
+                cbuf.rollout(t % H, actions[t:t + E])
+            else:
+                cbuf.step(t % H, actions[t])
         cbuf.carry_over()
     else:
         for t in range(W):
@@ -413,8 +421,12 @@ def measure_rollout(args, layout, world, rank, dev):
         if compact:
             if c:
                 cbuf.carry_over()
-            for j in range(H):
-                cbuf.step(j, actions[W + c * H + j])
+            if fused:                                    # one launch per refill epoch
+                for j in range(0, H, E):
+                    cbuf.rollout(j, actions[W + c * H + j:W + c * H + j + E])
+            else:
+                for j in range(H):
+                    cbuf.step(j, actions[W + c * H + j])
         else:
             for j in range(H):
                 eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
@@ -478,6 +490,17 @@ def measure_rollout(args, layout, world, rank, dev):
     # the refill beside the steps for as long as it runs (an event pair around every launch would
     # keep consecutive launches from overlapping at all).
     windows, cur = [], None
+    if fused:
+        # one window per launch (one refill epoch of E steps); the previous epoch's refill is joined
+        # before the window opens, so the window holds the epoch's fork (ring_pub copy) and the kernel
+        for t in range(0, P - P % E, E):
+            eng.join()
+            w = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), E]
+            w[0].record(stream)
+            cbuf.rollout(t % H, actions[W + K + t:W + K + t + E])
+            w[1].record(stream)
+            windows.append(w)
+        P = 0
 
     def probe_step(t):
         if compact:
@@ -530,12 +553,14 @@ def measure_rollout(args, layout, world, rank, dev):
         b_alg = B_STEP * n + (3 * args.size ** 2 + 208) * resets_per_launch
         achieved = b_alg / per_launch_s / 1e9
         traffic = None
-        pmc_file = PMC_FILE_COMPACT if compact else PMC_FILE
+        pmc_file = PMC_FILE_FUSED if fused else (PMC_FILE_COMPACT if compact else PMC_FILE)
         if os.path.exists(pmc_file):
             try:
                 pmc = json.load(open(pmc_file))
                 if pmc.get("n_envs") == n and pmc.get("size") == args.size and pmc.get("mission") == mission:
                     traffic = pmc.get("hbm_bytes_per_launch")
+                    if traffic is not None:                  # per step (a fused launch holds several)
+                        traffic = traffic / pmc.get("steps_per_launch", 1)
             except (OSError, ValueError):
                 traffic = None
         # VecFrameStack image + direction roll (reported separately); the compact layout rolls nothing
@@ -560,6 +585,8 @@ def measure_rollout(args, layout, world, rank, dev):
             "data": "synthetic (uniform random actions on {0..6}, seed 1234+rank; env i seeded 42+i; "
                     "synthetic values for GAE)",
             "config": {"workload": _workload_name(args, mission, n, world) + (
+                           " [fused rollout: one launch per %d-step refill epoch, observation rows into the rollout "
+                           "buffer]" % E if fused else
                            " [compact layout: observation rows into the rollout buffer]" if compact else ""),
                        "problem": args.problem, "mission": mission, "size": args.size, "num_objects": 4,
                        "envs_per_gpu": n, "n_stack": args.n_stack, "parallelism": "env-sharded dp%d" % world,
@@ -573,7 +600,10 @@ def measure_rollout(args, layout, world, rank, dev):
                        "gae_launches": nchunks},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
-                         "kernel": ("mgx_step_kernel<int, true> (compact)" if compact else "mgx_step_kernel<int, false> (SB3 stacks)"),
+                         "kernel": ("mgx_rollout_kernel<false> (fused: %d steps per launch; per-step figures = "
+                                    "launch / %d)" % (E, E) if fused else
+                                    "mgx_step_kernel<int, true> (compact)" if compact else
+                                    "mgx_step_kernel<int, false> (SB3 stacks)"),
                          "avg_launch_us": per_launch_s * 1e6,
                          "probe_launches": len(probe_us),
                          "step_pipeline_us": float(gpu_ms) * 1e3 / K,

@@ -188,6 +188,29 @@ typedef struct mgx_compact_out {
 mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_bytes, const mgx_compact_out *out,
                             void *stream);
 
+/* K consecutive mgx_step_compact calls fused into ONE launch, for a rollout whose actions are
+ * known up front (random-action or scripted rollouts: BASELINE config 2's workload; a policy in the
+ * loop needs mgx_step_compact per step).  actions_dev: int32 [K][N].  The outputs of step t go to
+ * row t of the [K][N] arrays below; terminal rows, ep_return, ep_len and livelock are left as
+ * after the last step.  Transitions, RNG streams, auto-resets, refill epochs and counters are
+ * those of the K calls, bit for bit.  The K steps must lie within one refill epoch:
+ * (mgx_step calls so far % refill_every) + K <= refill_every.  Needs the ring. */
+typedef struct mgx_rollout_out {
+    uint8_t *rows_dev;            /* u8 [K][N][148]: the observation after step t at row t */
+    uint8_t *mission_ids_dev;     /* u8 [K][N] */
+    uint8_t *terminal_row_dev;    /* u8 [N][148] (as mgx_compact_out) */
+    float *rewards_dev;           /* f32 [K][N] */
+    double *rewards64_dev;        /* f64 [K][N] (optional) */
+    uint8_t *terminated_dev;      /* u8 [K][N] */
+    uint8_t *truncated_dev;       /* u8 [K][N] */
+    uint8_t *dones_dev;           /* u8 [K][N] */
+    float *ep_return_dev;         /* f32 [N] (optional) */
+    int32_t *ep_len_dev;          /* i32 [N] (optional) */
+    int32_t *livelock_dev;        /* i32 [N] (optional) */
+} mgx_rollout_out;
+mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K, const mgx_rollout_out *out,
+                               void *stream);
+
 /* The current observation of every env as compact rows (e.g. row 0 after mgx_reset). */
 mgx_status mgx_observe_compact(mgx_handle *h, uint8_t *row_dev, uint8_t *mission_id_dev, void *stream);
 

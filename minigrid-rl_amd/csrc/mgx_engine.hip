@@ -470,6 +470,87 @@ __device__ __forceinline__ void render_cols(const uint8_t *grids, int S, int le,
     }
 }
 
+// One env's MiniGridEnv.step + PlaygroundEnv.step (custom_env.py:269-330), as selects: every
+// action's outcome is computed and the taken one kept (a branch per action made a divergent tree of
+// exec-mask updates -- half of the phase's instructions were SALU mask bookkeeping).  The front
+// cell is read from, and (pickup / drop / toggle) written to, env slot `le`'s chunk-major LDS grid.
+struct StepRes {
+    double rew;                       // the step's reward (Python float)
+    uint32_t view;                    // ax | ay<<8 | dir<<16 | carry<<24: what gen_obs() saw -- before
+                                      // PlaygroundEnv's key consumption (Q3)
+    int sc, mdone, rs;                // step count, mission_done, stored-reward step (-1 = None)
+    uint8_t carry;                    // carried object after the key consumption (Q4)
+    bool term, trunc, done, dirty;    // dirty: the grid changed
+};
+__device__ __forceinline__ StepRes env_step(const EnvState &st, int a, uint8_t *grids, int le, int S, int manual,
+                                            uint64_t mrange) {
+    StepRes R;
+    const int ms = S * S;
+    const int sc = st.step_count + 1;
+    int ax = st.ax, ay = st.ay, dir = st.dir;
+    uint8_t carry = st.carry;
+    const int fx = ax + ((dir == 0) - (dir == 2)), fy = ay + ((dir == 1) - (dir == 3));
+    uint8_t *fp = grids + cm_off(le, fy * S + fx);
+    const uint8_t fc = *fp;
+    const int ft = fc & 15;
+    // MiniGridEnv.step (3P)
+    const bool isF = a == A_FORWARD, isT = a == A_TOGGLE;
+    const int fcol = (fc >> 4) & 7;
+    dir = (dir + (a == A_RIGHT) + 3 * (a == A_LEFT)) & 3;
+    const bool mv = isF && can_overlap(fc);
+    ax = mv ? fx : ax;
+    ay = mv ? fy : ay;
+    const bool goal = isF && ft == T_GOAL;
+    const bool t0 = goal || (isF && ft == T_LAVA);
+    const bool pick = a == A_PICKUP && can_pickup(fc) && carry == 0;
+    const bool drop = a == A_DROP && ft == T_EMPTY && carry != 0;
+    // toggle: a locked door opens only with a Key of its colour; an open door closes; a box turns
+    // into its contents (the key it holds, or nothing)
+    const bool t_door = isT && ft == T_DOOR && (!(fc >> 7) || ((carry & 15) == T_KEY && ((carry >> 4) & 7) == fcol));
+    const bool t_open = isT && ft == T_OPEN, t_box = isT && ft == T_BOX;
+    uint8_t nc = fc;
+    nc = t_door ? mk_code(T_OPEN, fcol, 0) : nc;
+    nc = t_open ? mk_code(T_DOOR, fcol, 0) : nc;
+    nc = t_box ? ((fc >> 7) ? mk_code(T_KEY, fcol, 0) : CODE_EMPTY) : nc;
+    nc = pick ? CODE_EMPTY : nc;
+    nc = drop ? carry : nc;
+    carry = pick ? fc : (drop ? (uint8_t)0 : carry);
+    R.dirty = pick || drop || t_door || t_open || t_box;
+    if (R.dirty) *fp = nc;
+    R.trunc = sc >= ms;
+    R.view = (uint32_t)ax | ((uint32_t)ay << 8) | ((uint32_t)dir << 16) | ((uint32_t)carry << 24);
+    // ---- PlaygroundEnv.step (custom_env.py:269-330)
+    const int md0 = st.mission_done, rs0 = st.reward_step;
+    const bool is_gtg = st.mission_id == CMD_GOTOGOAL;
+    // Q4: toggling a door while carrying anything of its colour consumes it (not on a terminating step)
+    if (!t0 && isT && is_door(nc) && carry != 0 && ((nc >> 4) & 7) == ((carry >> 4) & 7)) carry = 0;
+    // mission completed this step (each test only sets `reward_step` if unset, `done` flag)
+    const int ta = st.target_action;
+    const bool has_t = st.tx != NONE8, ta_fwd = ta != NONE8 && ta != 0;
+    const int nfx = ax + ((dir == 0) - (dir == 2)), nfy = ay + ((dir == 1) - (dir == 3));
+    // (bitwise & / |: short-circuit operators turned this into a nest of branches)
+    const bool at_f = (nfx == st.tx) & (nfy == st.ty), at_a = (ax == st.tx) & (ay == st.ty);
+    const bool hit = (!t0 & !md0) &
+                     ((has_t & ta_fwd & at_f & (a == ta)) | (has_t & !ta_fwd & at_a) |
+                      (!has_t & (ta != NONE8) & (a == ta)) |
+                      ((st.mission_id >= MID_MOVE) & in_move_range(mrange, ax, ay)));
+    const int md1 = hit ? 1 : md0, rs1 = (hit && rs0 < 0) ? sc : rs0;
+    // 'done': the stored self.reward, or 0 -- in manual mode only a completed mission ends
+    const bool dn = !t0 && a == A_DONE && (md1 || !manual);
+    // reward: reaching the goal pays 1 - 0.9 sc/ms only on 'go to goal' missions; 'done' pays the
+    // reward stored at mission completion
+    double rew = 0.0;
+    if ((goal && is_gtg) || (dn && md1)) rew = reward_at(t0 ? sc : rs1, ms);
+    R.rew = rew;
+    R.mdone = t0 ? (is_gtg ? md0 : 0) : (dn ? 0 : md1);
+    R.rs = t0 ? (is_gtg ? rs0 : -1) : (dn ? -1 : rs1);
+    R.term = t0 || dn;
+    R.done = R.term || R.trunc;
+    R.sc = sc;
+    R.carry = carry;
+    return R;
+}
+
 // One vectorised env step of 64 envs per 256-thread workgroup.  No RNG work
 // happens here: auto-resets pop pre-generated episodes from the env's ring
 // (mgx_refill_kernel); an empty ring defers the env to mgx_fixup_kernel, which
@@ -658,73 +739,14 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     if (tid < ne) {
         const int64_t e = e0 + tid;
         if ((unsigned)a > 6u) { my_err |= MGX_DEVERR_BAD_ACTION; a = -1; }
-        const int ms = S * S;
-        const int sc = st.step_count + 1;
-        int ax = st.ax, ay = st.ay;
-        dir = st.dir;
-        uint8_t carry = st.carry;
-        const int fx = ax + ((dir == 0) - (dir == 2)), fy = ay + ((dir == 1) - (dir == 3));
-        uint8_t *fp = s_grid + cm_off(tid, fy * S + fx);
-        const uint8_t fc = *fp;
-        const int ft = fc & 15;
-        // MiniGridEnv.step (3P), as selects: every action's outcome is computed and the taken
-        // one kept (a branch per action made a divergent tree of exec-mask updates -- half of
-        // this phase's instructions were SALU mask bookkeeping)
-        const bool isF = a == A_FORWARD, isT = a == A_TOGGLE;
-        const int fcol = (fc >> 4) & 7;
-        dir = (dir + (a == A_RIGHT) + 3 * (a == A_LEFT)) & 3;
-        const bool mv = isF && can_overlap(fc);
-        ax = mv ? fx : ax;
-        ay = mv ? fy : ay;
-        const bool goal = isF && ft == T_GOAL;
-        term = goal || (isF && ft == T_LAVA);
-        const bool pick = a == A_PICKUP && can_pickup(fc) && carry == 0;
-        const bool drop = a == A_DROP && ft == T_EMPTY && carry != 0;
-        // toggle: a locked door opens only with a Key of its colour; an open door closes; a
-        // box turns into its contents (the key it holds, or nothing)
-        const bool t_door = isT && ft == T_DOOR &&
-                            (!(fc >> 7) || ((carry & 15) == T_KEY && ((carry >> 4) & 7) == fcol));
-        const bool t_open = isT && ft == T_OPEN, t_box = isT && ft == T_BOX;
-        uint8_t nc = fc;
-        nc = t_door ? mk_code(T_OPEN, fcol, 0) : nc;
-        nc = t_open ? mk_code(T_DOOR, fcol, 0) : nc;
-        nc = t_box ? ((fc >> 7) ? mk_code(T_KEY, fcol, 0) : CODE_EMPTY) : nc;
-        nc = pick ? CODE_EMPTY : nc;
-        nc = drop ? carry : nc;
-        carry = pick ? fc : (drop ? (uint8_t)0 : carry);
-        dirty = pick || drop || t_door || t_open || t_box;
-        if (dirty) *fp = nc;
-        trunc = sc >= ms;
-        // gen_obs() is taken here, before PlaygroundEnv's key consumption (Q3)
-        s_rp[tid] = (uint32_t)ax | ((uint32_t)ay << 8) | ((uint32_t)dir << 16) | ((uint32_t)carry << 24);
-        // ---- PlaygroundEnv.step (custom_env.py:269-330), as selects
-        const int md0 = st.mission_done, rs0 = st.reward_step;
-        const bool is_gtg = st.mission_id == CMD_GOTOGOAL;
-        const bool t0 = term;
-        // Q4: toggling a door while carrying a key of its colour consumes the key (not on a
-        // terminating step)
-        if (!t0 && isT && is_door(nc) && carry != 0 && ((nc >> 4) & 7) == ((carry >> 4) & 7)) carry = 0;
-        // mission completed this step (each test only sets `reward_step` if unset, `done` flag)
-        const int ta = st.target_action;
-        const bool has_t = st.tx != NONE8, ta_fwd = ta != NONE8 && ta != 0;
-        const int nfx = ax + ((dir == 0) - (dir == 2)), nfy = ay + ((dir == 1) - (dir == 3));
-        // (bitwise & / |: short-circuit operators turned this into a nest of branches)
-        const bool at_f = (nfx == st.tx) & (nfy == st.ty), at_a = (ax == st.tx) & (ay == st.ty);
-        const bool hit = (!t0 & !md0) &
-                         ((has_t & ta_fwd & at_f & (a == ta)) | (has_t & !ta_fwd & at_a) |
-                          (!has_t & (ta != NONE8) & (a == ta)) |
-                          ((st.mission_id >= MID_MOVE) & in_move_range(mrange, ax, ay)));
-        const int md1 = hit ? 1 : md0, rs1 = (hit && rs0 < 0) ? sc : rs0;
-        // 'done': the stored self.reward, or 0 -- in manual mode only a completed mission ends
-        const bool dn = !t0 && a == A_DONE && (md1 || !p.manual);
-        // reward: reaching the goal pays 1 - 0.9 sc/ms only on 'go to goal' missions; 'done'
-        // pays the reward stored at mission completion
-        double rew = 0.0;
-        if ((goal && is_gtg) || (dn && md1)) rew = reward_at(t0 ? sc : rs1, ms);
-        mdone = t0 ? (is_gtg ? md0 : 0) : (dn ? 0 : md1);
-        rs = t0 ? (is_gtg ? rs0 : -1) : (dn ? -1 : rs1);
-        term = t0 || dn;
-        done = term || trunc;
+        const StepRes r = env_step(st, a, s_grid, tid, S, p.manual, mrange);
+        const int ax = r.view & 0xFF, ay = (r.view >> 8) & 0xFF;
+        const uint8_t carry = r.carry;
+        dir = (r.view >> 16) & 3;
+        s_rp[tid] = r.view;
+        const double rew = r.rew;
+        const int sc = r.sc;
+        term = r.term; trunc = r.trunc; done = r.done; dirty = r.dirty; mdone = r.mdone; rs = r.rs;
         // the episode ends (auto-reset) only on 'forward' into goal / lava, on 'done' or at the time
         // limit, each of which implies `spec`: the next episode is already in LDS (phase 1e)
         const bool avail = done && spec;
@@ -1078,6 +1100,275 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         atomicAdd(&p.counters[7], ts4 - ts2);   // phase 3+5: stack roll + grid write-back
 #endif
 #endif
+    }
+}
+
+// ======================================================= fused rollout kernel
+// mgx_rollout_compact: K consecutive compact steps -- mgx_step_compact's transition, RNG streams,
+// auto-resets and outputs, bit for bit -- of 64 envs per workgroup in ONE launch, for a rollout
+// whose actions are known up front (a random-action or scripted rollout: BASELINE config 2's
+// workload).  The per-step kernel is bound by latency, not bytes: its 1,024 workgroups all start
+// together, so all of them wait on the same two load round trips (state, then the popped episode),
+// then compute, then store, in lock-step.  Here the env state stays in registers and
+// LDS between steps: a step loads nothing it must wait for -- its actions and the episodes it may
+// pop are prefetched a step ahead by a fifth, DMA-only wave -- and the workgroups drift apart, so
+// one's stores drain under another's step logic and render.
+//   waves 0-3  as mgx_step_kernel<., true>: wave 0 = one lane per env (env_step), then all four
+//              render 4 threads per env and copy their 16 rows out
+//   wave 4     LDS-DMA only (never waits on a store): actions of step t+1; for an env that popped at
+//              step t-1, its ring episode after next.  Every env keeps its next TWO ring episodes
+//              staged (buffer = ring position & 1), so a pop never waits.
+// Outputs of step t go to row t of [K][N] arrays; the env state, ring head and grids are written
+// back once, at the end.  The refill may run concurrently (it reads ring_head once, at its start:
+// a stale head only under-estimates its free slots); the K steps lie within one refill epoch, whose
+// join published >= K episodes per env, so every staged slot is in [head, pub).
+struct ROut {
+    uint8_t *rows, *mids, *t_rows;   // [K][N][148], [K][N], [N][148]
+    float *reward;                   // [K][N]
+    double *reward64;                // [K][N] (optional)
+    uint8_t *term, *trunc, *done;    // [K][N]
+    float *ep_ret;                   // [N] as after the last step (optional)
+    int32_t *ep_len, *livelock;      // [N] as after the last step (optional)
+};
+constexpr int ROLL_THREADS = BLOCK_THREADS + 64;
+
+template <bool VIS>   // see_through_walls == False (Grid.process_vis): its code only in the variant that needs it
+__global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p, ROut o, const int32_t *__restrict__ actions,
+                                                                      int K) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr int CSTK = (BLOCK_ENVS * FROW + 15) & ~15;
+    const int GSQ = p.GS >> 4, GB = GSQ * BLOCK_ENVS * 16;
+    uint8_t *s_stk = smem;                                             // frame rows [64][148]
+    uint8_t *s_grid = smem + CSTK;                                     // current grids (chunk-major, cm_off)
+    uint8_t *s_pg = s_grid + GB;                                       // [2] staged ring episodes' grids
+    uint4 *s_ph = reinterpret_cast<uint4 *>(s_pg + 2 * GB);            // [2][64] their headers
+    uint4 *s_pr = s_ph + 2 * BLOCK_ENVS;                               // [2][2][64] their RNG snapshots
+    int32_t *s_act = reinterpret_cast<int32_t *>(s_pr + 4 * BLOCK_ENVS);   // [2][64] actions
+    __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params of the frame written (post-step view or
+                                                 // the popped episode's first)
+    __shared__ uint32_t s_rpt[BLOCK_ENVS];       // post-step view of a finished episode (terminal row)
+    __shared__ uint8_t s_term[BLOCK_ENVS];       // terminal row written this step
+    __shared__ uint8_t s_popb[BLOCK_ENVS];       // staged buffer popped this step (0xFF: none)
+    __shared__ uint8_t s_nh[2][BLOCK_ENVS];      // [step & 1] new ring head of an env that popped (0xFF: none)
+    __shared__ unsigned long long s_tmask;
+    // per-env state between steps lives in LDS, not registers: a loop-carried value would stay live
+    // through the render, where the register pressure peaks (in registers: 128 VGPRs, 3 workgroups
+    // per CU instead of 4)
+    __shared__ uint4 s_st[BLOCK_ENVS];           // EnvState
+    __shared__ uint8_t s_head[BLOCK_ENVS], s_pub[BLOCK_ENVS];
+    __shared__ unsigned long long s_mr[BLOCK_ENVS];   // 'move' target_range (problems mov / full)
+    __shared__ unsigned long long s_cnt[2];      // resets, abandoned attempts
+    __shared__ uint32_t s_err;
+
+    const int tid = threadIdx.x, lane = tid & (BLOCK_ENVS - 1);
+    const int64_t e0 = (int64_t)blockIdx.x * BLOCK_ENVS;
+    const int64_t N = p.n;
+    const int ne = (int)min<int64_t>(BLOCK_ENVS, N - e0);
+    const int S = p.S, D = p.D;
+    const bool wave0 = tid < BLOCK_ENVS, dmaw = tid >= BLOCK_THREADS;
+    const int lc = min(lane, ne - 1);
+    // ---- setup: ring positions and state (waves 0 and 4), grids (waves 0-3, LDS-DMA)
+    if (wave0) {
+        s_st[lane] = reinterpret_cast<const uint4 *>(p.state)[e0 + lc];
+        s_head[lane] = p.ring_head[e0 + lc];
+        s_pub[lane] = p.ring_pub[e0 + lc];
+        s_mr[lane] = p.range_cur[p.has_move ? e0 + lc : 0];
+        s_nh[1][lane] = 0xFF;
+        if (lane < 2) s_cnt[lane] = 0;
+        if (lane == 0) s_err = 0;
+    }
+    if (!dmaw) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.grid + (e0 + lc) * p.GS);
+        for (int c = tid >> 6; c < GSQ; c += BLOCK_THREADS / 64)
+            __builtin_amdgcn_global_load_lds(src + c, s_grid + c * (BLOCK_ENVS * 16), 16, 0, 0);
+    }
+    // stage ring episode h of env e (this lane's) into buffer h & 1: header, RNG snapshot, grid
+    auto stage = [&](uint8_t h) {
+        const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + (h & (D - 1));   // 32-bit offsets: fewer VGPRs
+        const uint4 *hs = p.ring_hdr + 3 * slot, *rs = p.ring_rng + 2 * slot;
+        const uint4 *gs = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
+        if (h & 1) {                                 // LDS-DMA destinations must be wave-uniform
+            __builtin_amdgcn_global_load_lds(hs, s_ph + BLOCK_ENVS, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(rs, s_pr + 2 * BLOCK_ENVS, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(rs + 1, s_pr + 3 * BLOCK_ENVS, 16, 0, 0);
+            for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + GB + c * (BLOCK_ENVS * 16), 16, 0, 0);
+        } else {
+            __builtin_amdgcn_global_load_lds(hs, s_ph, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(rs, s_pr, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(rs + 1, s_pr + BLOCK_ENVS, 16, 0, 0);
+            for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + c * (BLOCK_ENVS * 16), 16, 0, 0);
+        }
+    };
+    if (dmaw && lane < ne) {
+        __builtin_amdgcn_global_load_lds(actions + e0 + lane, s_act, 4, 0, 0);
+        const uint8_t rhead = p.ring_head[e0 + lane], rpub = p.ring_pub[e0 + lane];
+        const int q = (uint8_t)(rpub - rhead);
+        if (q > 0) stage(rhead);
+        if (q > 1) stage((uint8_t)(rhead + 1));
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+
+    for (int t = 0; t < K; t++) {
+        const int tb = t & 1;
+        if (dmaw) {
+            // the next step's actions; the ring episode after next of every env that popped last step
+            if (lane < ne) {
+                if (t + 1 < K)
+                    __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lane, s_act + (tb ^ 1) * BLOCK_ENVS,
+                                                     4, 0, 0);
+                const uint8_t nh = s_nh[tb ^ 1][lane];
+                if (nh != 0xFF && (uint8_t)(s_pub[lane] - nh) > 1) stage((uint8_t)(nh + 1));
+            }
+        } else if (wave0) {
+            // ---- the step: one lane per env
+            bool tw = false;
+            uint8_t popb = 0xFF, nh = 0xFF;
+            if (lane < ne) {
+                const uint32_t e = (uint32_t)(e0 + lane), oi = (uint32_t)t * (uint32_t)N + e;   // N * K < 2^32
+                EnvState st;
+                {
+                    const uint4 sv = s_st[lane];
+                    __builtin_memcpy(&st, &sv, sizeof st);
+                }
+                uint8_t rhead = s_head[lane];
+                uint64_t mrange = p.has_move ? s_mr[lane] : 0ull;
+                uint32_t err = 0;
+                int a = s_act[tb * BLOCK_ENVS + lane];
+                if ((unsigned)a > 6u) { err |= MGX_DEVERR_BAD_ACTION; a = -1; }
+                const StepRes r = env_step(st, a, s_grid, lane, S, p.manual, mrange);
+                tw = r.done && (p.terminal_mode == MGX_TERMINAL_ALL ||
+                                (p.terminal_mode == MGX_TERMINAL_TRUNCATED && r.trunc && !r.term));
+                s_rpt[lane] = r.view;
+                o.reward[oi] = (float)r.rew;
+                if (o.reward64) o.reward64[oi] = r.rew;
+                o.term[oi] = r.term;
+                o.trunc[oi] = r.trunc;
+                o.done[oi] = r.done;
+                if (t == K - 1) {
+                    if (o.ep_ret) o.ep_ret[e] = (float)r.rew;    // only the final step can pay a reward
+                    if (o.ep_len) o.ep_len[e] = r.sc;
+                }
+                uint8_t mid = st.mission_id;
+                int lvl = 0;
+                if (r.done && (uint8_t)(s_pub[lane] - rhead) != 0) {
+                    // SubprocVecEnv auto-reset: the staged ring episode (header, RNG snapshot, grid)
+                    popb = rhead & 1;
+                    const uint4 h = s_ph[popb * BLOCK_ENVS + lane];
+                    p.cur_rng[2 * e] = s_pr[(2 * popb) * BLOCK_ENVS + lane];
+                    p.cur_rng[2 * e + 1] = s_pr[(2 * popb + 1) * BLOCK_ENVS + lane];
+                    if (p.has_move) s_mr[lane] = p.ring_range[e * (uint32_t)D + (rhead & (D - 1))];
+                    mid = (uint8_t)(h.y >> 16);
+                    st.ax = (uint8_t)(h.x & 0xFF); st.ay = (uint8_t)((h.x >> 8) & 0xFF); st.dir = (uint8_t)((h.x >> 16) & 0xFF);
+                    st.carry = 0; st.step_count = 0; st.reward_step = (int16_t)r.rs;     // survives the reset (Q2)
+                    st.tx = (uint8_t)(h.x >> 24); st.ty = (uint8_t)h.y; st.target_action = (uint8_t)(h.y >> 8);
+                    st.mission_id = mid; st.mission_done = (uint8_t)r.mdone; st.frames = 1; st.flags = 0; st.pad = 0;
+                    s_rp[lane] = h.x & 0xFFFFFFu;
+                    rhead++;
+                    s_head[lane] = rhead;
+                    nh = rhead;
+                    atomicAdd(&s_cnt[0], 1ull);
+                    if (h.z) atomicAdd(&s_cnt[1], (unsigned long long)h.z);
+                    lvl = (int)h.z;
+                } else {
+                    if (r.done) err |= MGX_DEVERR_RING_EMPTY;   // cannot happen (refill production rule)
+                    st.ax = (uint8_t)(r.view & 0xFF); st.ay = (uint8_t)((r.view >> 8) & 0xFF);
+                    st.dir = (uint8_t)((r.view >> 16) & 3); st.carry = r.carry;
+                    st.step_count = (uint16_t)r.sc; st.reward_step = (int16_t)r.rs; st.mission_done = (uint8_t)r.mdone;
+                    s_rp[lane] = r.view;
+                }
+                o.mids[oi] = mid;
+                if (t == K - 1 && o.livelock) o.livelock[e] = lvl;
+                {
+                    uint4 sv;
+                    __builtin_memcpy(&sv, &st, sizeof st);
+                    s_st[lane] = sv;
+                }
+                if (err) atomicOr(&s_err, err);
+            }
+            s_term[lane] = tw;
+            s_popb[lane] = popb;
+            s_nh[tb][lane] = nh;
+            const unsigned long long tm = __ballot(tw);
+            if (lane == 0) s_tmask = tm;
+        }
+        __syncthreads();
+        // (every barrier below is reached by all five waves: the DMA wave's threads have le >= 64)
+        const int le = tid >> 2, q = tid & 3;
+        if (s_tmask) {
+            // terminal rows (rare, block-uniform): the finished episode's last view, rendered into the
+            // env's frame row from its post-step grid and copied out before the row is reused below
+            if (le < ne && s_term[le]) render_cols(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW + 1);
+            __syncthreads();
+            if (VIS) {
+                if (tid < ne && s_term[tid]) apply_vis(s_stk + tid * FROW + 1);
+                __syncthreads();
+            }
+            if (tid < ne && s_term[tid]) s_stk[tid * FROW] = (uint8_t)((s_rpt[tid] >> 16) & 3);
+            __syncthreads();
+            if (le < ne && s_term[le]) {
+                const uint32_t *fr = reinterpret_cast<const uint32_t *>(s_stk + le * FROW);
+                uint32_t *tr = reinterpret_cast<uint32_t *>(o.t_rows + (e0 + le) * (int64_t)FROW);
+#pragma unroll 1
+                for (int k = 10 * q; k < min(10 * q + 10, FROW / 4); k++) tr[k] = fr[k];
+            }
+            __syncthreads();
+        }
+        // the frame of every env: the new episode's first where one was popped (rendered straight from
+        // its staged grid, which then becomes the env's grid)
+        if (le < ne) {
+            const uint8_t b = s_popb[le];
+            const uint8_t *g = b == 0xFF ? s_grid : s_pg + b * GB;
+            const uint32_t rp = s_rp[le];
+            render_cols(g, S, le, q, rp, s_stk + le * FROW + 1);
+            if (q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);
+            if (b != 0xFF)
+                for (int c = q; c < GSQ; c += 4)
+                    *reinterpret_cast<uint4 *>(s_grid + c * (BLOCK_ENVS * 16) + le * 16) =
+                        *reinterpret_cast<const uint4 *>(g + c * (BLOCK_ENVS * 16) + le * 16);
+        }
+        if (VIS) {
+            __syncthreads();
+            if (tid < ne) apply_vis(s_stk + tid * FROW + 1);
+            __syncthreads();
+        }
+        if (!dmaw) {
+            // rows out: per wave (its 16 rows, no barrier) or, after process_vis, per block
+            const bool wave_rows = !VIS;
+            const int r0 = wave_rows ? (tid >> 6) * 16 : 0;
+            const int nr = wave_rows ? max(0, min(16, ne - r0)) : ne;
+            const int tt = wave_rows ? lane : tid, nt = wave_rows ? 64 : BLOCK_THREADS;
+            if (wave_rows) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            const int nb16 = (nr * FROW) >> 4;
+            const uint4 *src = reinterpret_cast<const uint4 *>(s_stk + r0 * FROW);
+            uint4 *dst = reinterpret_cast<uint4 *>(o.rows + ((int64_t)t * N + e0 + r0) * FROW);
+            for (int i = tt; i < nb16; i += nt) dst[i] = src[i];
+            const int rem = ((nr * FROW) >> 2) - (nb16 << 2);
+            if (tt < rem)
+                reinterpret_cast<uint32_t *>(dst + nb16)[tt] = reinterpret_cast<const uint32_t *>(src + nb16)[tt];
+        }
+        // the DMA wave: this step's prefetches have landed before the next step reads them
+        if (dmaw) __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
+    // ---- write back: state and ring head (wave 0), every grid, counters
+    if (wave0 && lane < ne) {
+        reinterpret_cast<uint4 *>(p.state)[e0 + lane] = s_st[lane];
+        p.ring_head[e0 + lane] = s_head[lane];
+        if (p.has_move) p.range_cur[e0 + lane] = s_mr[lane];
+    }
+    if (!dmaw) {
+        uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * p.GS);
+        for (int i = tid; i < ne * GSQ; i += BLOCK_THREADS) {
+            const int le = i / GSQ, c = i - le * GSQ;
+            dst[i] = *reinterpret_cast<const uint4 *>(s_grid + c * (BLOCK_ENVS * 16) + le * 16);
+        }
+    }
+    if (tid == 0) {
+        atomicAdd(&p.blk[blockIdx.x].x, (unsigned long long)ne * (unsigned long long)K);
+        if (s_cnt[0]) atomicAdd(&p.blk[blockIdx.x].y, s_cnt[0]);
+        if (s_cnt[1]) atomicAdd(&p.blk[blockIdx.x].z, s_cnt[1]);
+        if (s_err) atomicOr(p.err, s_err);
     }
 }
 
@@ -1847,7 +2138,7 @@ struct mgx_handle {
     mgx_config cfg;
     int device;
     KParams kp;
-    size_t lds_step, lds_step_compact, lds_reset, lds_refill;
+    size_t lds_step, lds_step_compact, lds_reset, lds_refill, lds_rollout;
     int nw;                 // 64-bit words of the generator's S*S cell masks (1, 2 or 4)
     bool ext;               // generator variant with full / drp / mov / obstacles
     int refill_every;       // K: steps per refill epoch
@@ -2145,6 +2436,11 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
                           + (size_t)BLOCK_ENVS * 3 * 16;                                     // + popped header, RNG snapshot
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
+    // fused rollout: frame rows + current grids + two staged ring episodes (grid, header, RNG) + actions
+    h->lds_rollout = (size_t)((BLOCK_ENVS * FROW + 15) & ~15) + (size_t)BLOCK_ENVS * 3 * GS +
+                     (size_t)BLOCK_ENVS * 6 * 16 + (size_t)2 * BLOCK_ENVS * 4;
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
     h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
     h->ext = cfg->obstacles || cfg->problem == MGX_PROBLEM_FULL || cfg->problem == MGX_PROBLEM_DRP ||
              cfg->problem == MGX_PROBLEM_MOV;
@@ -2397,6 +2693,47 @@ mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_b
                            (hipStream_t)stream, h->kp, o, (const int64_t *)actions_dev);
     HIP_TRY(hipGetLastError());
     h->calls++;
+    return MGX_OK;
+}
+
+mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K, const mgx_rollout_out *out,
+                               void *stream) {
+    if (!h || !out || !actions_dev) return fail(MGX_ERR_INVALID, "mgx_rollout_compact: null argument");
+    if (!out->rows_dev || !out->mission_ids_dev || !out->rewards_dev || !out->terminated_dev || !out->truncated_dev ||
+        !out->dones_dev)
+        return fail(MGX_ERR_INVALID, "mgx_rollout_compact: missing output buffer");
+    if (h->kp.terminal_mode != MGX_TERMINAL_NONE && !out->terminal_row_dev)
+        return fail(MGX_ERR_INVALID, "mgx_rollout_compact: terminal_mode needs terminal_row_dev");
+    if (h->kp.D == 0) return fail(MGX_ERR_INVALID, "mgx_rollout_compact: needs the episode ring (ring_depth >= 0)");
+    const uint64_t E = (uint64_t)h->refill_every;
+    if (K < 1 || (h->calls % E) + (uint64_t)K > E)
+        return fail(MGX_ERR_INVALID, "mgx_rollout_compact: the K steps must lie within one refill epoch "
+                                     "((calls % refill_every) + K <= refill_every)");
+    ROut o;
+    o.rows = out->rows_dev;
+    o.mids = out->mission_ids_dev;
+    o.t_rows = out->terminal_row_dev;
+    o.reward = out->rewards_dev;
+    o.reward64 = out->rewards64_dev;
+    o.term = out->terminated_dev;
+    o.trunc = out->truncated_dev;
+    o.done = out->dones_dev;
+    o.ep_ret = out->ep_return_dev;
+    o.ep_len = out->ep_len_dev;
+    o.livelock = out->livelock_dev;
+    if (h->calls % E == 0) {
+        mgx_status fs = fork_refill(h, stream);
+        if (fs != MGX_OK) return fs;
+    }
+    const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
+    if (h->kp.vis)
+        hipLaunchKernelGGL(mgx_rollout_kernel<true>, dim3((unsigned)nblk), dim3(ROLL_THREADS), h->lds_rollout,
+                           (hipStream_t)stream, h->kp, o, actions_dev, K);
+    else
+        hipLaunchKernelGGL(mgx_rollout_kernel<false>, dim3((unsigned)nblk), dim3(ROLL_THREADS), h->lds_rollout,
+                           (hipStream_t)stream, h->kp, o, actions_dev, K);
+    HIP_TRY(hipGetLastError());
+    h->calls += (uint64_t)K;
     return MGX_OK;
 }
 

@@ -25,7 +25,7 @@ DEVERR = {1: "MT19937 ring: a cursor left the window of the stream the device ho
 # Every entry point include/mgx.h declares (checked by tests/test_abi.py).
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
            "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_gae_dones", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text",
-           "mgx_step_compact", "mgx_observe_compact", "mgx_gather", "mgx_scene")
+           "mgx_step_compact", "mgx_rollout_compact", "mgx_observe_compact", "mgx_gather", "mgx_scene")
 
 
 class MgxConfig(ctypes.Structure):
@@ -64,6 +64,15 @@ class MgxCompactOut(ctypes.Structure):
     ]
 
 
+class MgxRolloutOut(ctypes.Structure):
+    _fields_ = [
+        ("rows_dev", ctypes.c_void_p), ("mission_ids_dev", ctypes.c_void_p), ("terminal_row_dev", ctypes.c_void_p),
+        ("rewards_dev", ctypes.c_void_p), ("rewards64_dev", ctypes.c_void_p), ("terminated_dev", ctypes.c_void_p),
+        ("truncated_dev", ctypes.c_void_p), ("dones_dev", ctypes.c_void_p), ("ep_return_dev", ctypes.c_void_p),
+        ("ep_len_dev", ctypes.c_void_p), ("livelock_dev", ctypes.c_void_p),
+    ]
+
+
 class MgxError(RuntimeError):
     pass
 
@@ -99,6 +108,7 @@ def load():
     L.mgx_mission_text.argtypes = [I, ctypes.c_char_p, ctypes.c_size_t]
     L.mgx_step_compact.argtypes = [P, P, I, ctypes.POINTER(MgxCompactOut), P]
     L.mgx_observe_compact.argtypes = [P, P, P, P]
+    L.mgx_rollout_compact.argtypes = [P, P, I, ctypes.POINTER(MgxRolloutOut), P]
     L.mgx_gather.argtypes = [P, P, P, P, I64, P, I64, P, P, I, P, I, P, P]
     L.mgx_scene.argtypes = [P, I64, ctypes.POINTER(ctypes.c_uint32), P]
     for name in EXPORTS:

@@ -83,6 +83,34 @@ class CompactBuffer:
                    "mgx_step_compact")
         e.calls += 1
 
+    def rollout(self, t, actions):
+        """K = len(actions) steps in ONE launch (mgx_rollout_compact): actions int32 [K, N] known up
+        front (a random-action or scripted rollout); observations t+1 .. t+K, rewards / dones of
+        steps t .. t+K-1 -- the same as K step() calls, bit for bit.  The K steps must lie within one
+        refill epoch of the engine."""
+        e = self.engine
+        K = int(actions.shape[0])
+        if actions.device != e.device or actions.dtype != torch.int32 or tuple(actions.shape) != (K, self.N) \
+                or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous int32 [K, %d] tensor on %s" % (self.N, e.device))
+        if t < 0 or t + K > self.T:
+            raise ValueError("steps %d..%d outside the buffer's %d" % (t, t + K - 1, self.T))
+        r = self.row(t + 1)
+        o = _lib.MgxRolloutOut()
+        o.rows_dev = self.rows[r].data_ptr()
+        o.mission_ids_dev = self.mids[r].data_ptr()
+        o.terminal_row_dev = self.terminal_rows.data_ptr()
+        o.rewards_dev = self.rewards[t].data_ptr()
+        o.rewards64_dev = None
+        o.terminated_dev = self.terminated[t].data_ptr()
+        o.truncated_dev = self.truncated[t].data_ptr()
+        o.dones_dev = self.starts[r].data_ptr()
+        o.ep_return_dev = e.ep_return.data_ptr()
+        o.ep_len_dev = e.ep_len.data_ptr()
+        o.livelock_dev = e.livelock.data_ptr()
+        _lib.check(e.L.mgx_rollout_compact(e.h, _ptr(actions), K, ctypes.byref(o), e._stream()), "mgx_rollout_compact")
+        e.calls += K
+
     def carry_over(self):
         """Start the next rollout: its history rows and observation 0 are this one's last rows."""
         src = slice(self.T, self.T + self.H + 1)

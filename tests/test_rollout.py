@@ -1,0 +1,211 @@
+"""The fused rollout (mgx_rollout_compact: K compact steps in one launch, mgx/compact.py
+CompactBuffer.rollout) against the per-step kernel and the C oracle: every step's observation row,
+mission id, reward, done / terminated / truncated flags, the terminal rows, the counters and the
+engine state after every chunk must equal K mgx_step_compact calls bit for bit (which are pinned to
+the reference fixtures, test_gpu_parity.py), and the C oracle directly at BASELINE sizes."""
+import numpy as np
+import pytest
+
+import trajcheck as TC
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _engines(kw, n, **ekw):
+    from mgx import MgxEngine
+    from mgx.compact import CompactBuffer
+    a = MgxEngine(n_envs=n, terminal_mode="all", mission_dtype=torch.uint8, reward64=False, **kw, **ekw)
+    b = MgxEngine(n_envs=n, terminal_mode="all", mission_dtype=torch.uint8, reward64=False, **kw, **ekw)
+    return a, b
+
+
+CASES = [dict(problem="multi", mission=5, size=8, n=4096),                     # config 2's GTG
+         dict(problem="multi", mission=None, size=8, n=1000),                  # ragged last workgroup
+         dict(problem="multi", mission=1, size=16, n=300),
+         dict(problem="multi", mission=1, size=16, n=130, see_through_walls=False),
+         dict(problem="multi", mission=2, size=11, n=257, all_doors_open=True),
+         dict(problem="mov", mission=None, size=8, n=200),                     # 'move' target ranges
+         dict(problem="multi", mission=None, size=8, n=512, manual=True)]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "_".join("%s%s" % (k[:3], v) for k, v in c.items()))
+@pytest.mark.parametrize("chunks", [(32,), (5, 11, 16)], ids=["epoch", "split"])
+def test_rollout_equals_per_step(case, chunks):
+    """Two engines of one config and seed: one steps per call (mgx_step_compact), the other runs the
+    same actions in fused chunks (a whole refill epoch, or an epoch split 5 + 11 + 16) -- over
+    several epochs with the buffer carried over, every output and the final state equal."""
+    _need_gpu()
+    from mgx.compact import CompactBuffer
+    kw = dict(case)
+    n = kw.pop("n")
+    E = 32
+    ref, fus = _engines(kw, n, refill_every=E)
+    assert ref.refill_every == E and sum(chunks) == E
+    T = 2 * E
+    br, bf = CompactBuffer(ref, T), CompactBuffer(fus, T)
+    ref.reset(); fus.reset()
+    br.observe(0); bf.observe(0)
+    g = torch.Generator(device=ref.device)
+    g.manual_seed(9)
+    for rollout in range(3):
+        if rollout:
+            br.carry_over(); bf.carry_over()
+        acts = torch.randint(0, 7, (T, n), device=ref.device, generator=g, dtype=torch.int32)
+        if rollout == 1:
+            acts[3:9] = 6                                     # bursts of 'done': pops on consecutive steps
+        t = 0
+        while t < T:
+            for k in chunks:
+                bf.rollout(t, acts[t:t + k].contiguous())
+                for j in range(k):
+                    br.step(t + j, acts[t + j])
+                t += k
+                assert torch.equal(br.terminal_rows, bf.terminal_rows), (rollout, t)
+        for name in ("rows", "mids", "starts", "rewards", "terminated", "truncated"):
+            assert torch.equal(getattr(br, name), getattr(bf, name)), (rollout, name)
+        for name in ("ep_return", "ep_len", "livelock"):
+            assert torch.equal(getattr(ref, name), getattr(fus, name)), (rollout, name)
+    ref.poll_error()
+    fus.poll_error()
+    a, b = ref.dump_state(), fus.dump_state()
+    for k in a:
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k
+    sa, sb = ref.stats(), fus.stats()
+    # ('queued' may differ: the refill reads each ring head once, at its start, concurrently with the
+    # steps -- per-step calls may already have advanced some heads, the fused kernel writes them at its
+    # end; both keep >= K episodes queued at every join, DESIGN §4.3.  What is produced -- and so the
+    # producer-side max MT cursor -- is a prefix of the same episode sequence either way; the
+    # consumed episodes are the same.)
+    for k in ("steps", "resets", "livelocks", "calls"):
+        assert sa[k] == sb[k], (k, sa, sb)
+    assert sb["queued"] >= E * n, sb
+
+
+@pytest.mark.parametrize("problem,mission,size,n,T", [("multi", 5, 8, 65536, 64), ("multi", 1, 16, 131072, 32)],
+                         ids=["cfg2_65536", "cfg5_131072"])
+def test_rollout_full_size_matches_oracle(problem, mission, size, n, T):
+    """BASELINE per-GPU sizes: the fused rollout of T steps (whole refill epochs) against the C
+    oracle -- every env's row, done flag and f32 reward at every step, then every env's state."""
+    _need_gpu()
+    import oracle as O
+    from mgx import MgxEngine
+    from mgx._lib import mission_tokens
+    from mgx.compact import CompactBuffer
+    E = 32
+    ov = O.OracleVec(problem, mission, size, 4, n, 42)
+    eng = MgxEngine(problem=problem, mission=mission, size=size, n_envs=n, terminal_mode="truncated",
+                    mission_dtype=torch.uint8, refill_every=E)
+    buf = CompactBuffer(eng, T)
+    tok = mission_tokens()
+    ov.reset()
+    eng.reset()
+    buf.observe(0)
+    acts = np.random.default_rng(2024).integers(0, 7, (T, n)).astype(np.int32)
+    ad = torch.as_tensor(acts, device=eng.device)
+    for t in range(0, T, E):
+        buf.rollout(t, ad[t:t + E].contiguous())
+    torch.cuda.synchronize()
+    rows, mids = buf.rows.cpu().numpy(), buf.mids.cpu().numpy()
+    starts, rew = buf.starts.cpu().numpy().astype(bool), buf.rewards.cpu().numpy()
+    H = buf.H
+    for t in range(T):
+        o = ov.step(acts[t])
+        done = (o["terminated"] | o["truncated"]).astype(bool)
+        r = rows[H + 1 + t]
+        img = r[:, 1:].reshape(n, 3, 7, 7).transpose(0, 2, 3, 1)
+        assert np.array_equal(starts[H + 1 + t], done), t
+        assert np.array_equal(img, np.where(done[:, None, None, None], o["r_image"], o["image"])), t
+        assert np.array_equal(r[:, 0], np.where(done, o["r_dir"], o["dir"])), t
+        assert np.array_equal(tok[mids[H + 1 + t]], np.where(done[:, None], o["r_mission"], o["mission"])), t
+        assert np.array_equal(rew[t], o["reward"].astype(np.float32)), t
+    a, b = eng.dump_state(), ov.dump()
+    for k in ("grid", "agent", "carrying", "step_count", "mission_done", "mtwords", "pcg", "target"):
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a["stored_reward"], b["stored_reward"], equal_nan=True)
+    eng.poll_error()
+
+
+@pytest.mark.parametrize("path", TC.fixtures(), ids=lambda p: p.split("/")[-1][:-4])
+def test_rollout_matches_reference_fixture(path):
+    """Every reference fixture through the fused rollout in whole epochs of 16 steps: each step's
+    observation (the terminal frame where the episode ended, from the terminal row of that chunk when
+    it is the env's last ending in it), reward, flags and new-episode observation; at every chunk end
+    the env state."""
+    _need_gpu()
+    from mgx import MgxEngine
+    from mgx._lib import mission_tokens
+    from mgx.compact import CompactBuffer
+    d = dict(np.load(path))
+    cfg, T = TC.fixture_cfg(d)
+    kw = dict(cfg)
+    n = kw.pop("n_envs")
+    E = 16
+    eng = MgxEngine(n_envs=n, terminal_mode="all", mission_dtype=torch.uint8, refill_every=E, **kw)
+    buf = CompactBuffer(eng, T)
+    tok = mission_tokens()
+    eng.reset()
+    buf.observe(0)
+    H = buf.H
+    r0 = buf.rows[H].cpu().numpy()
+    assert np.array_equal(r0[:, 1:].reshape(n, 3, 7, 7).transpose(0, 2, 3, 1), d["reset0_image"])
+    acts = torch.as_tensor(d["actions"].astype(np.int32), device=eng.device)
+    for c in range(T // E):
+        t0 = c * E
+        buf.rollout(t0, acts[t0:t0 + E].contiguous())
+        torch.cuda.synchronize()
+        rows, mids = buf.rows.cpu().numpy(), buf.mids.cpu().numpy()
+        starts, rew = buf.starts.cpu().numpy().astype(bool), buf.rewards.cpu().numpy()
+        trm, trc = buf.terminated.cpu().numpy(), buf.truncated.cpu().numpy()
+        trows = buf.terminal_rows.cpu().numpy()
+        last_end = np.full(n, -1)
+        for t in range(t0, t0 + E):
+            done = (d["terminated"][t] | d["truncated"][t]).astype(bool)
+            last_end[done] = t
+            r = rows[H + 1 + t]
+            img = r[:, 1:].reshape(n, 3, 7, 7).transpose(0, 2, 3, 1)
+            assert np.array_equal(starts[H + 1 + t], done), t
+            assert np.array_equal(trm[t], d["terminated"][t]) and np.array_equal(trc[t], d["truncated"][t]), t
+            assert np.array_equal(rew[t], d["reward"][t].astype(np.float32)), t
+            assert np.array_equal(img[~done], d["image"][t][~done]), t
+            assert np.array_equal(img[done], d["r_image"][t][done]), t
+            assert np.array_equal(r[~done, 0], d["dir"][t][~done]) and np.array_equal(r[done, 0], d["r_dir"][t][done]), t
+            assert np.array_equal(tok[mids[H + 1 + t]][~done], d["mission"][t][~done]), t
+            assert np.array_equal(tok[mids[H + 1 + t]][done], d["r_mission"][t][done]), t
+        for i in np.nonzero(last_end >= 0)[0]:                      # the chunk's last terminal row per env
+            t = last_end[i]
+            got = trows[i, 1:].reshape(3, 7, 7).transpose(1, 2, 0)
+            assert np.array_equal(got, d["image"][t][i]) and trows[i, 0] == d["dir"][t][i], (t, i)
+        st = eng.dump_state()
+        t = t0 + E - 1
+        done = (d["terminated"][t] | d["truncated"][t]).astype(bool)
+        for k in TC.STATE_KEYS:
+            assert np.array_equal(st[k][~done], d[k][t][~done]), (t, k)
+        for k in ("grid", "agent", "mtwords", "pcg", "target"):
+            assert np.array_equal(st[k][done], d["r_" + k][t][done]), (t, k)
+        assert np.array_equal(st["mission_done"], d["mission_done"][t]), t
+        assert np.array_equal(st["stored_reward"], d["stored_reward"][t], equal_nan=True), t
+    eng.poll_error()
+
+
+def test_rollout_rejects_chunks_across_epochs():
+    _need_gpu()
+    from mgx import MgxEngine, MgxError
+    from mgx.compact import CompactBuffer
+    eng = MgxEngine(problem="multi", mission=5, size=8, n_envs=128, refill_every=16, mission_dtype=torch.uint8)
+    buf = CompactBuffer(eng, 64)
+    eng.reset()
+    buf.observe(0)
+    a = torch.zeros((64, 128), dtype=torch.int32, device=eng.device)
+    buf.rollout(0, a[:10].contiguous())
+    with pytest.raises(MgxError, match="refill epoch"):
+        buf.rollout(10, a[10:20].contiguous())          # 10 + 10 > 16
+    buf.rollout(10, a[10:16].contiguous())
+    buf.rollout(16, a[16:32].contiguous())
+    eng.poll_error()
