@@ -73,7 +73,9 @@ constexpr int MT_SB_GROUPS = MT_SB_WORDS / MT_FIELDS;
 constexpr int MT_SLIDE_MAX_SB = 64;                       // super-blocks one slide generates at most (200 k words)
 constexpr unsigned long long MT_AHEAD = 1ull << 19;       // words kept generated past the furthest producer cursor
 constexpr long long MT_HOST_FILL = 1ll << 20;             // words the host generates at create
-constexpr int SLIDE_THREADS = 1024, SLIDE_ENVS = 4 * SLIDE_THREADS;
+// 256 threads: the slider must find room on a CU beside the step / rollout kernels (a 1,024-thread
+// workgroup waited ~50 us for a whole CU behind the fused rollout, and the refill waited behind it)
+constexpr int SLIDE_THREADS = 256, SLIDE_ENVS = 16 * SLIDE_THREADS;
 // LDS bytes per resetting lane: MT window + objs list (obj_stride words, see mgx_create)
 __host__ __device__ constexpr int scratch_per_env(int obj_stride) { return WIN_STRIDE * 4 + obj_stride * 4; }
 
@@ -1211,35 +1213,41 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
 
     for (int t = 0; t < K; t++) {
         const int tb = t & 1;
+        // thread index through an opaque copy: lane- / env-derived addresses are then computed inside
+        // each region of the step, instead of being hoisted out of the loop and kept live through all of
+        // them (96 -> fewer VGPRs; the render's and the step logic's registers no longer add up)
+        int tidv = tid;
+        asm volatile("" : "+v"(tidv));
+        const int lanev = tidv & (BLOCK_ENVS - 1);
         if (dmaw) {
             // the next step's actions; the ring episode after next of every env that popped last step
-            if (lane < ne) {
+            if (lanev < ne) {
                 if (t + 1 < K)
-                    __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lane, s_act + (tb ^ 1) * BLOCK_ENVS,
+                    __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lanev, s_act + (tb ^ 1) * BLOCK_ENVS,
                                                      4, 0, 0);
-                const uint8_t nh = s_nh[tb ^ 1][lane];
-                if (nh != 0xFF && (uint8_t)(s_pub[lane] - nh) > 1) stage((uint8_t)(nh + 1));
+                const uint8_t nh = s_nh[tb ^ 1][lanev];
+                if (nh != 0xFF && (uint8_t)(s_pub[lanev] - nh) > 1) stage((uint8_t)(nh + 1));
             }
         } else if (wave0) {
-            // ---- the step: one lane per env
+            // ---- the step: one lanev per env
             bool tw = false;
             uint8_t popb = 0xFF, nh = 0xFF;
-            if (lane < ne) {
-                const uint32_t e = (uint32_t)(e0 + lane), oi = (uint32_t)t * (uint32_t)N + e;   // N * K < 2^32
+            if (lanev < ne) {
+                const uint32_t e = (uint32_t)(e0 + lanev), oi = (uint32_t)t * (uint32_t)N + e;   // N * K < 2^32
                 EnvState st;
                 {
-                    const uint4 sv = s_st[lane];
+                    const uint4 sv = s_st[lanev];
                     __builtin_memcpy(&st, &sv, sizeof st);
                 }
-                uint8_t rhead = s_head[lane];
-                uint64_t mrange = p.has_move ? s_mr[lane] : 0ull;
+                uint8_t rhead = s_head[lanev];
+                uint64_t mrange = p.has_move ? s_mr[lanev] : 0ull;
                 uint32_t err = 0;
-                int a = s_act[tb * BLOCK_ENVS + lane];
+                int a = s_act[tb * BLOCK_ENVS + lanev];
                 if ((unsigned)a > 6u) { err |= MGX_DEVERR_BAD_ACTION; a = -1; }
-                const StepRes r = env_step(st, a, s_grid, lane, S, p.manual, mrange);
+                const StepRes r = env_step(st, a, s_grid, lanev, S, p.manual, mrange);
                 tw = r.done && (p.terminal_mode == MGX_TERMINAL_ALL ||
                                 (p.terminal_mode == MGX_TERMINAL_TRUNCATED && r.trunc && !r.term));
-                s_rpt[lane] = r.view;
+                s_rpt[lanev] = r.view;
                 o.reward[oi] = (float)r.rew;
                 if (o.reward64) o.reward64[oi] = r.rew;
                 o.term[oi] = r.term;
@@ -1251,21 +1259,21 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 }
                 uint8_t mid = st.mission_id;
                 int lvl = 0;
-                if (r.done && (uint8_t)(s_pub[lane] - rhead) != 0) {
+                if (r.done && (uint8_t)(s_pub[lanev] - rhead) != 0) {
                     // SubprocVecEnv auto-reset: the staged ring episode (header, RNG snapshot, grid)
                     popb = rhead & 1;
-                    const uint4 h = s_ph[popb * BLOCK_ENVS + lane];
-                    p.cur_rng[2 * e] = s_pr[(2 * popb) * BLOCK_ENVS + lane];
-                    p.cur_rng[2 * e + 1] = s_pr[(2 * popb + 1) * BLOCK_ENVS + lane];
-                    if (p.has_move) s_mr[lane] = p.ring_range[e * (uint32_t)D + (rhead & (D - 1))];
+                    const uint4 h = s_ph[popb * BLOCK_ENVS + lanev];
+                    p.cur_rng[2 * e] = s_pr[(2 * popb) * BLOCK_ENVS + lanev];
+                    p.cur_rng[2 * e + 1] = s_pr[(2 * popb + 1) * BLOCK_ENVS + lanev];
+                    if (p.has_move) s_mr[lanev] = p.ring_range[e * (uint32_t)D + (rhead & (D - 1))];
                     mid = (uint8_t)(h.y >> 16);
                     st.ax = (uint8_t)(h.x & 0xFF); st.ay = (uint8_t)((h.x >> 8) & 0xFF); st.dir = (uint8_t)((h.x >> 16) & 0xFF);
                     st.carry = 0; st.step_count = 0; st.reward_step = (int16_t)r.rs;     // survives the reset (Q2)
                     st.tx = (uint8_t)(h.x >> 24); st.ty = (uint8_t)h.y; st.target_action = (uint8_t)(h.y >> 8);
                     st.mission_id = mid; st.mission_done = (uint8_t)r.mdone; st.frames = 1; st.flags = 0; st.pad = 0;
-                    s_rp[lane] = h.x & 0xFFFFFFu;
+                    s_rp[lanev] = h.x & 0xFFFFFFu;
                     rhead++;
-                    s_head[lane] = rhead;
+                    s_head[lanev] = rhead;
                     nh = rhead;
                     atomicAdd(&s_cnt[0], 1ull);
                     if (h.z) atomicAdd(&s_cnt[1], (unsigned long long)h.z);
@@ -1275,36 +1283,36 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                     st.ax = (uint8_t)(r.view & 0xFF); st.ay = (uint8_t)((r.view >> 8) & 0xFF);
                     st.dir = (uint8_t)((r.view >> 16) & 3); st.carry = r.carry;
                     st.step_count = (uint16_t)r.sc; st.reward_step = (int16_t)r.rs; st.mission_done = (uint8_t)r.mdone;
-                    s_rp[lane] = r.view;
+                    s_rp[lanev] = r.view;
                 }
                 o.mids[oi] = mid;
                 if (t == K - 1 && o.livelock) o.livelock[e] = lvl;
                 {
                     uint4 sv;
                     __builtin_memcpy(&sv, &st, sizeof st);
-                    s_st[lane] = sv;
+                    s_st[lanev] = sv;
                 }
                 if (err) atomicOr(&s_err, err);
             }
-            s_term[lane] = tw;
-            s_popb[lane] = popb;
-            s_nh[tb][lane] = nh;
+            s_term[lanev] = tw;
+            s_popb[lanev] = popb;
+            s_nh[tb][lanev] = nh;
             const unsigned long long tm = __ballot(tw);
-            if (lane == 0) s_tmask = tm;
+            if (lanev == 0) s_tmask = tm;
         }
         __syncthreads();
         // (every barrier below is reached by all five waves: the DMA wave's threads have le >= 64)
-        const int le = tid >> 2, q = tid & 3;
+        const int le = tidv >> 2, q = tidv & 3;
         if (s_tmask) {
             // terminal rows (rare, block-uniform): the finished episode's last view, rendered into the
             // env's frame row from its post-step grid and copied out before the row is reused below
             if (le < ne && s_term[le]) render_cols(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW + 1);
             __syncthreads();
             if (VIS) {
-                if (tid < ne && s_term[tid]) apply_vis(s_stk + tid * FROW + 1);
+                if (tidv < ne && s_term[tidv]) apply_vis(s_stk + tidv * FROW + 1);
                 __syncthreads();
             }
-            if (tid < ne && s_term[tid]) s_stk[tid * FROW] = (uint8_t)((s_rpt[tid] >> 16) & 3);
+            if (tidv < ne && s_term[tidv]) s_stk[tidv * FROW] = (uint8_t)((s_rpt[tidv] >> 16) & 3);
             __syncthreads();
             if (le < ne && s_term[le]) {
                 const uint32_t *fr = reinterpret_cast<const uint32_t *>(s_stk + le * FROW);
@@ -1329,15 +1337,15 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         }
         if (VIS) {
             __syncthreads();
-            if (tid < ne) apply_vis(s_stk + tid * FROW + 1);
+            if (tidv < ne) apply_vis(s_stk + tidv * FROW + 1);
             __syncthreads();
         }
         if (!dmaw) {
             // rows out: per wave (its 16 rows, no barrier) or, after process_vis, per block
             const bool wave_rows = !VIS;
-            const int r0 = wave_rows ? (tid >> 6) * 16 : 0;
+            const int r0 = wave_rows ? (tidv >> 6) * 16 : 0;
             const int nr = wave_rows ? max(0, min(16, ne - r0)) : ne;
-            const int tt = wave_rows ? lane : tid, nt = wave_rows ? 64 : BLOCK_THREADS;
+            const int tt = wave_rows ? lanev : tidv, nt = wave_rows ? 64 : BLOCK_THREADS;
             if (wave_rows) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             const int nb16 = (nr * FROW) >> 4;
             const uint4 *src = reinterpret_cast<const uint4 *>(s_stk + r0 * FROW);
@@ -1624,19 +1632,21 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t x) {
     const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
     return x ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
-__device__ __forceinline__ void mt_twist_block(uint32_t *s, int tid) {
+__device__ __forceinline__ void mt_twist_block(uint32_t *s, int tid) {   // >= 227 threads
     uint32_t v = 0;
     if (tid < 227) v = mt_mix(s[tid], s[tid + 1], s[tid + 397]);
     __syncthreads();
     if (tid < 227) s[tid] = v;
     __syncthreads();
-    if (tid >= 227 && tid < 454) v = mt_mix(s[tid], s[tid + 1], s[tid - 227]);
+    const int i = 227 + tid;
+    if (tid < 227) v = mt_mix(s[i], s[i + 1], s[i - 227]);
     __syncthreads();
-    if (tid >= 227 && tid < 454) s[tid] = v;
+    if (tid < 227) s[i] = v;
     __syncthreads();
-    if (tid >= 454 && tid < 624) v = mt_mix(s[tid], s[tid == 623 ? 0 : tid + 1], s[tid - 227]);
+    const int k = 454 + tid;
+    if (tid < 170) v = mt_mix(s[k], s[k == 623 ? 0 : k + 1], s[k - 227]);
     __syncthreads();
-    if (tid >= 454 && tid < 624) s[tid] = v;
+    if (tid < 170) s[k] = v;
     __syncthreads();
 }
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
@@ -1663,7 +1673,7 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     MtCtl *c = p.mtc;
     unsigned long long mn = ~0ull, mx = 0;
     const int64_t e0 = (int64_t)blockIdx.x * SLIDE_ENVS;
-#pragma unroll
+#pragma unroll 4
     for (int k = 0; k < SLIDE_ENVS / SLIDE_THREADS; k++) {
         const int64_t e = e0 + k * SLIDE_THREADS + tid;
         if (e < p.n) {
@@ -1722,14 +1732,15 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     for (int sb = 0; sb < nsb; sb++) {
         for (int b = 0; b < MT_SB_WORDS / 624; b++) {
             mt_twist_block(s_st, tid);
-            if (tid < 624) s_f[b * 624 + tid] = (uint8_t)(mt_temper(s_st[tid]) >> 27);   // getrandbits(k<=5) field
+            for (int i = tid; i < 624; i += SLIDE_THREADS)
+                s_f[b * 624 + i] = (uint8_t)(mt_temper(s_st[i]) >> 27);   // getrandbits(k<=5) field
         }
         __syncthreads();
-        if (tid < MT_SB_GROUPS) {
+        for (int gi = tid; gi < MT_SB_GROUPS; gi += SLIDE_THREADS) {
             uint64_t grp = 0;
 #pragma unroll
-            for (int k = 0; k < MT_FIELDS; k++) grp |= (uint64_t)s_f[tid * MT_FIELDS + k] << (6 * k);
-            const uint64_t slot = (hi + (unsigned long long)tid) & p.mt_mask;
+            for (int k = 0; k < MT_FIELDS; k++) grp |= (uint64_t)s_f[gi * MT_FIELDS + k] << (6 * k);
+            const uint64_t slot = (hi + (unsigned long long)gi) & p.mt_mask;
             p.mt[slot] = grp;
             if (slot < (uint64_t)MT_PAD) p.mt[p.mt_mask + 1 + slot] = grp;   // mirror: windows stay contiguous
         }
