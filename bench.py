@@ -552,17 +552,22 @@ def measure_rollout(args, layout, world, rank, dev):
         resets_per_launch = (st1["resets"] - st0["resets"]) / K
         b_alg = B_STEP * n + (3 * args.size ** 2 + 208) * resets_per_launch
         achieved = b_alg / per_launch_s / 1e9
-        traffic = None
-        pmc_file = PMC_FILE_FUSED if fused else (PMC_FILE_COMPACT if compact else PMC_FILE)
-        if os.path.exists(pmc_file):
+        traffic, traffic_src = None, None
+        # rocprofv3 PMC HBM bytes of this kernel at this config (tools/gpu_r3_profiles.sh -> profiles/r03_pmc/)
+        import glob
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r03_pmc", "pmc_[0-9]_%s.json" % layout)))
+        cands += [PMC_FILE_FUSED if fused else (PMC_FILE_COMPACT if compact else PMC_FILE)]
+        for pmc_file in cands:
             try:
                 pmc = json.load(open(pmc_file))
-                if pmc.get("n_envs") == n and pmc.get("size") == args.size and pmc.get("mission") == mission:
-                    traffic = pmc.get("hbm_bytes_per_launch")
-                    if traffic is not None:                  # per step (a fused launch holds several)
-                        traffic = traffic / pmc.get("steps_per_launch", 1)
             except (OSError, ValueError):
-                traffic = None
+                continue
+            if pmc.get("n_envs") == n and pmc.get("size") == args.size and pmc.get("mission") == mission:
+                traffic = pmc.get("hbm_bytes_per_launch")
+                if traffic is not None:                  # per step (a fused launch holds several)
+                    traffic = traffic / pmc.get("steps_per_launch", 1)
+                    traffic_src = os.path.relpath(pmc_file, ROOT)
+                break
         # VecFrameStack image + direction roll (reported separately); the compact layout rolls nothing
         stack_bytes = 0 if compact else n * (441 + 588 + 12 + 16)
         out = {
@@ -599,7 +604,7 @@ def measure_rollout(args, layout, world, rank, dev):
                        "episodes_consumed": st1["resets"] - st0["resets"],
                        "gae_launches": nchunks},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
+                         "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": ("mgx_rollout_kernel<false> (fused: %d steps per launch; per-step figures = "
                                     "launch / %d)" % (E, E) if fused else
                                     "mgx_step_kernel<int, true> (compact)" if compact else

@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--size", type=int, default=8)
     ap.add_argument("--eval-episodes", type=int, default=1000)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--max-seconds", type=float, default=0, help="stop training after this long (then evaluate)")
+    ap.add_argument("--progress", default=None, help="append one JSON line per rollout here")
     args = ap.parse_args()
     from mgx.ppo import PPOConfig, learn
     env_kw = dict(problem="multi", mission=args.mission, size=args.size, num_objects=4)
@@ -62,13 +64,21 @@ def main():
     t0 = time.perf_counter()
     curve = []
 
+    class Stop:                                        # SB3-style callback: False ends learn()
+        def on_step(self, policy, num_timesteps):
+            return not (args.max_seconds and time.perf_counter() - t0 > args.max_seconds)
+
     def log(st):
         if "timesteps" in st:
             curve.append({k: st[k] for k in ("timesteps", "ep_rew_mean", "ep_len_mean", "lr", "kl", "clipfrac")})
+            curve[-1]["seconds"] = time.perf_counter() - t0
+            if args.progress:
+                with open(args.progress, "a") as f:
+                    f.write(json.dumps(curve[-1]) + "\n")
             if len(curve) % 10 == 1:
                 print("t=%.0fs %s" % (time.perf_counter() - t0, json.dumps(curve[-1])), file=sys.stderr, flush=True)
     random_eval = success_rate(None, env_kw, args.eval_episodes, seed=4242)
-    pol, hist, eng = learn(cfg, int(args.timesteps), log=log)
+    pol, hist, eng = learn(cfg, int(args.timesteps), log=log, callback=Stop())
     train_s = time.perf_counter() - t0
     eng.close()
     ev = success_rate(pol, env_kw, args.eval_episodes, seed=4242)
