@@ -124,6 +124,7 @@ struct KParams {
     int initial_fill;       // this refill launch is mgx_reset's (fill every ring to 2K)
     int reset_mode;         // mgx_reset: 0 first (seeded, MT cursor 0), 1 seeded, 2 unseeded
     int step_prio;          // s_setprio of the step kernel's waves (env MGX_STEP_PRIO, 0..3)
+    int refill_prio;        // s_setprio of the refill's waves (env MGX_REFILL_PRIO, 0..3)
     int prod_mean;          // refill production per lane capped at the wave's mean deficit (env MGX_REFILL_MEAN)
     uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
                             //        generation (mgx_scene regenerates it), else null
@@ -1462,6 +1463,10 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     uint8_t *s_scr = smem + ((64 * p.GSL + 15) & ~15);        // [64] windows + objs
     unsigned long long maxcur = 0;
     uint32_t err = 0;
+    // issue priority over co-resident step / rollout waves (MGX_REFILL_PRIO; wave-uniform)
+    if (p.refill_prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (p.refill_prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (p.refill_prio == 3) __builtin_amdgcn_s_setprio(3);
 #ifdef MGX_REFILL_CLOCK
     const unsigned long long rc0 = __builtin_amdgcn_s_memtime();   // diagnostics: wave clocks per launch
     int rc_iters = 0;
@@ -2266,6 +2271,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         h->serial_refill = sv && sv[0] == '1';
         const char *st = std::getenv("MGX_STEP_PRIO");
         h->kp.step_prio = st ? std::atoi(st) : 0;
+        const char *rp = std::getenv("MGX_REFILL_PRIO");
+        h->kp.refill_prio = rp ? std::atoi(rp) : 0;
         const char *pm = std::getenv("MGX_REFILL_MEAN");
         h->kp.prod_mean = pm ? std::atoi(pm) : 1;
         const char *rg = std::getenv("MGX_REFILL_GENERIC");

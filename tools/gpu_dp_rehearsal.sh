@@ -1,0 +1,15 @@
+#!/bin/bash
+# Rehearsal of bench.py's N > 1 path on ONE GPU with the gloo backend (RCCL refuses two ranks on one
+# GPU; the driver's 8-GPU run uses RCCL): 2 and 4 ranks, each its own shard of 65,536 envs
+# (env_index_offset = rank * n), barrier + max-over-ranks timing, the adv-stat all-reduce per horizon,
+# ranks_seen from a collective.  Output lines -> gpurun_out/dp/.
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/dp
+mkdir -p $O
+for np in 2 4; do
+  MGX_DIST_BACKEND=gloo timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 --master-port $((29500 + np)) bench.py --gpus $np --steps 64 --warmup 5 --cpu-seconds 0 > $O/dp$np.json 2>$O/dp$np.err || { tail -20 $O/dp$np.err; exit 1; }
+  python -c "
+import json; d=json.load(open('$O/dp$np.json'))
+print('np $np n_gpus', d['n_gpus'], 'ranks_seen', d['ranks_seen'], 'backend', d['dist_backend'], 'value %.3e' % d['value'], d['config']['timed'])"
+done
