@@ -47,6 +47,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "minigrid-rl_amd"))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -73,6 +74,8 @@ def parse():
     ap.add_argument("--probe", type=int, default=256, help="eager steps timed per launch for the roofline")
     ap.add_argument("--workload", default="rollout", choices=["rollout", "ppo"])
     ap.add_argument("--refill-every", type=int, default=0, help="steps per refill epoch (0 = engine default, D/4)")
+    ap.add_argument("--min-warmup", type=int, default=2048,
+                    help="rollout: the warm-up is at least this many steps (whole refill epochs)")
     ap.add_argument("--refill-cap", type=int, default=0, help="extra episodes per env per epoch (0 = engine default)")
     ap.add_argument("--ring-depth", type=int, default=0, help="episode ring depth (0 = engine default)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
@@ -83,6 +86,8 @@ def parse():
                          "largest whole-epoch divisor of --steps up to 1024; ppo: default 16)")
     ap.add_argument("--batch-size", type=int, default=65536, help="ppo: minibatch size")
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
+    ap.add_argument("--eval-episodes", type=int, default=100,
+                    help="ppo: deterministic evaluate_policy episodes after the timed iterations (0: none)")
     ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layout")
     ap.add_argument("--layout", default=None, choices=["compact", "sb3", "fused"],
                     help="observation storage: compact rows + mgx_gather (mgx_step_compact, one launch per "
@@ -280,6 +285,11 @@ def main_ppo(args, world, rank, local, dev):
         wall = _allreduce(wall, dist.ReduceOp.MAX)
     eng.poll_error()
     wall = float(wall[0])
+    ev = None
+    if rank == 0 and args.eval_episodes > 0:          # untimed: learning evidence for the trained policy
+        ev = _ppo_success(pol, cfg.env, args.eval_episodes, dev)
+        ev["after"] = {"ppo_iterations": K + W, "env_steps": (K + W) * n * cfg.horizon * world,
+                       "optimizer_steps": (K + W) * cfg.n_epochs * max(1, n * world * cfg.horizon // cfg.batch_size)}
     if rank == 0:
         print(json.dumps({
             "metric": "PPO env-steps/sec (rollout + train), PKP 8x8, 65k envs/GPU",
@@ -295,10 +305,30 @@ def main_ppo(args, world, rank, local, dev):
                        "mission_cache": cfg.mission_cache, "layout": cfg.layout,
                        "parallelism": "env-sharded dp%d" % world},
             "phases_s_per_iter": {"collect": tc / K, "train": tt / K},
+            "eval": ev,
             "roofline": None,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _ppo_success(pol, env_kw, episodes, dev):
+    """evaluate_policy (mgx/evaluation.py, SB3's semantics) over `episodes` deterministic episodes
+    on a fresh engine (seed 4242): success = an episode that paid a reward (README.md:54-65's
+    "Benchmark (1k ep)" column; the reference quotes 57 % for its PKP model)."""
+    from mgx import MgxEngine, evaluate_policy
+    eng = MgxEngine(n_envs=episodes, seed=4242, n_stack=4, terminal_mode="none", reward64=True,
+                    mission_dtype=torch.uint8, device=dev, **env_kw)
+    was = pol.training
+    pol.train(False)
+    t0 = time.perf_counter()
+    rews, lens = evaluate_policy(pol, eng, episodes, deterministic=True, return_episode_rewards=True)
+    pol.train(was)
+    eng.close()
+    r = np.asarray(rews)
+    return {"episodes": int(r.size), "deterministic": True, "success_rate": float((r > 0).mean()),
+            "mean_reward": float(r.mean()), "mean_length": float(np.mean(lens)),
+            "seconds": round(time.perf_counter() - t0, 3)}
 
 
 def pick_epoch(K, D=128):
@@ -371,7 +401,7 @@ def measure_rollout(args, layout, world, rank, dev):
     # fill towards D at (cap - consumption) per env per epoch, ~1.3 episodes per 32 steps; a
     # shorter warm-up would time that fill-up (the refill producing more than the steps consume),
     # not the steady state, where production = consumption (`window` reports both)
-    W = -(-max(args.warmup, 2048) // E) * E
+    W = -(-max(args.warmup, args.min_warmup, 1) // E) * E
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     P = args.probe
