@@ -113,6 +113,7 @@ struct KParams {
     uint8_t *ring_head;     // [N] consumer (step kernel) position
     uint8_t *ring_tail;     // [N] producer (refill kernel) position
     uint8_t *ring_pub;      // [N] ring_tail as of the last join: the step kernel pops below it
+    uint8_t *ring_seen;     // [N] ring_head as the last refill read it (its consumption estimate)
     uint32_t *fix_list;     // [N] envs whose ring was empty at their reset (mgx_fixup_kernel)
     uint32_t *fix_count;    // list length; fix_done: workgroups of the fixup kernel that finished
     uint32_t *fix_done;
@@ -121,11 +122,12 @@ struct KParams {
     int D;
     int K;                  // refill epoch (steps)
     int cap;                // episodes an env produces per epoch beyond what the invariant needs (<0: fill to D)
-    int initial_fill;       // this refill launch is mgx_reset's (fill every ring to 2K)
+    int initial_fill;       // this refill launch is mgx_reset's (fill every ring to D)
     int reset_mode;         // mgx_reset: 0 first (seeded, MT cursor 0), 1 seeded, 2 unseeded
     int step_prio;          // s_setprio of the step kernel's waves (env MGX_STEP_PRIO, 0..3)
     int refill_prio;        // s_setprio of the refill's waves (env MGX_REFILL_PRIO, 0..3)
-    int prod_mean;          // refill production per lane capped at the wave's mean deficit (env MGX_REFILL_MEAN)
+    int prod_mean;          // refill production cap per wave (env MGX_REFILL_MEAN): 0 fixed `cap`,
+                            // 1 the wave's mean deficit (<= cap), 2 its mean consumption, rounded up
     uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
                             //        generation (mgx_scene regenerates it), else null
 };
@@ -402,6 +404,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
         store_rng(G, p, e);
         rng_snapshot(G, p.cur_rng + 2 * e);
         p.ring_head[e] = 0; p.ring_tail[e] = 0; p.ring_pub[e] = 0;   // empty ring (mgx_refill_kernel fills)
+        p.ring_seen[e] = 0;
         // stacked obs: zeros + first frame
         uint8_t *row = o.img + e * (int64_t)p.img_bytes;
         for (int k = 0; k < p.img_bytes - FRAME; k++) row[k] = 0;
@@ -1474,11 +1477,13 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     // The step kernel may be popping this env's ring concurrently: `head` can be stale
     // (older, smaller), which only under-estimates the free slots.
     uint8_t tail = 0;
-    int level = 0;
+    int level = 0, cons = 0;
     if (e < p.n) {
         const uint8_t head = *reinterpret_cast<volatile const uint8_t *>(p.ring_head + e);
         tail = p.ring_tail[e];
         level = (int)(uint8_t)(tail - head);
+        cons = (int)(uint8_t)(head - p.ring_seen[e]);    // episodes popped since the last refill read
+        p.ring_seen[e] = head;
     }
     const int space = p.D - level, need = 2 * p.K - level;
     // Production: at least what keeps >= K episodes queued at the next join (each step pops
@@ -1488,17 +1493,27 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     // wave's mean deficit (D - level, rounded), so the wave runs about as many attempt rounds as
     // its lanes consumed on average, not as many as its busiest lane did; a lane left behind
     // keeps its deficit, which raises the next epoch's mean (the ring depth absorbs it).
+    // prod_mean 2 (default): the cap is the wave's mean CONSUMPTION since the last refill, rounded
+    // up, so the wave runs about as many attempt rounds as its lanes popped on average: production
+    // keeps up with consumption (rounding up) while the lanes that popped more than the mean keep a
+    // deficit the ring depth absorbs.  A fixed cap must sit well above the mean (rounds = cap), and
+    // the mean-deficit cap (1) settles above it too (deficits grow until the cap covers the lanes).
     int cap = p.cap;
     if (p.prod_mean && cap > 0 && !p.initial_fill) {
-        int sum = e < p.n ? space : 0, cnt = e < p.n ? 1 : 0;
+        const bool by_cons = p.prod_mean == 2;
+        int sum = e < p.n ? (by_cons ? cons : space) : 0, cnt = e < p.n ? 1 : 0;
         for (int off = 32; off > 0; off >>= 1) {
             sum += __shfl_xor(sum, off);
             cnt += __shfl_xor(cnt, off);
         }
-        cap = min(cap, (2 * sum + cnt) / (2 * max(cnt, 1)));
+        cnt = max(cnt, 1);
+        cap = by_cons ? (sum + cnt - 1) / cnt : min(cap, (2 * sum + cnt) / (2 * cnt));
     }
     if (e < p.n) {
-        int nfree = p.initial_fill ? need : max(need, p.cap < 0 ? space : min(cap, space));
+        // mgx_reset's fill: every ring to D (not just the invariant's 2K), so the epochs that follow
+        // start at steady state: production then tracks consumption at once instead of running
+        // need-driven rounds until the rings have filled (1,500+ steps at a cap near consumption)
+        int nfree = p.initial_fill ? space : max(need, p.cap < 0 ? space : min(cap, space));
         nfree = min(nfree, space);
         int nmin = max(need, 0);                   // what the ring invariant requires this epoch
         if (nfree > 0) {
@@ -2274,7 +2289,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         const char *rp = std::getenv("MGX_REFILL_PRIO");
         h->kp.refill_prio = rp ? std::atoi(rp) : 0;
         const char *pm = std::getenv("MGX_REFILL_MEAN");
-        h->kp.prod_mean = pm ? std::atoi(pm) : 1;
+        h->kp.prod_mean = pm ? std::atoi(pm) : 2;
         const char *rg = std::getenv("MGX_REFILL_GENERIC");
         h->refill_multi = !(rg && rg[0] == '1');
     }
@@ -2304,12 +2319,12 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     }
     const int D = h->cfg.ring_depth;
     {
-        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 48, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 3 + 64};
+        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 48, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 4 + 64};
         for (int i = 0; i < 5; i++) {
             hipError_t e = hipMalloc(&h->allocs[7 + i], rs[i] ? rs[i] : 16);
             if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, std::string("hipMalloc ring: ") + hipGetErrorString(e)));
         }
-        hipError_t e = hipMemset(h->allocs[11], 0, (size_t)N * 3 + 64);
+        hipError_t e = hipMemset(h->allocs[11], 0, (size_t)N * 4 + 64);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset ring ctl"));
         e = hipMemset(h->allocs[10], 0, (size_t)N * 32);      // cursors read by the MT slider before any reset
         if (e == hipSuccess) e = hipMemset(h->allocs[3], 0, (size_t)N * 16);
@@ -2409,6 +2424,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.ring_head = (uint8_t *)h->allocs[11];
     p.ring_tail = p.ring_head + N;
     p.ring_pub = p.ring_head + 2 * N;
+    p.ring_seen = p.ring_head + 3 * N;
     p.fix_list = (uint32_t *)h->allocs[12];
     p.fix_count = p.fix_list + N + 4;       // 16-B aligned tail of the same allocation
     p.fix_done = p.fix_list + N + 8;
@@ -2527,7 +2543,7 @@ static mgx_status launch_slide(mgx_handle *h, void *stream) {
 static mgx_status launch_refill(mgx_handle *h, void *stream) {
     if (h->kp.D == 0) return MGX_OK;
     h->refill_launches++;
-    if (!h->kp.initial_fill) {               // (mgx_reset's fill starts where the reset kernel left the cursors)
+    {   // (mgx_reset's fill: from where the reset kernel left the cursors; D episodes ahead)
         mgx_status ss = launch_slide(h, stream);
         if (ss != MGX_OK) return ss;
     }
@@ -2611,7 +2627,7 @@ mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, v
     MGX_GEN_LAUNCH(mgx_reset_kernel, dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_reset, (hipStream_t)stream, h->kp, o);
     HIP_TRY(hipGetLastError());
     h->calls = 0;
-    h->kp.initial_fill = 1;                     // fills every ring to 2K (synchronously on `stream`)
+    h->kp.initial_fill = 1;                     // fills every ring to D (synchronously on `stream`)
     const mgx_status rs = launch_refill(h, stream);
     h->kp.initial_fill = 0;
     return rs;

@@ -484,9 +484,12 @@ def test_bench_shape_graph_matches_oracle(n):
 
 
 def test_refill_accounting():
-    """mgx_stats: pre-generated episodes queued in the rings.  mgx_reset fills every ring to 2K;
+    """mgx_stats: pre-generated episodes queued in the rings.  mgx_reset fills every ring to D
+    (less abandoned attempts);
     each epoch the refill tops the rings up so that >= K stay queued at its join,
-    never more than D; episodes produced in an epoch = resets consumed + change of the queue."""
+    never more than D; episodes produced in an epoch = resets consumed + change of the queue.
+    Production follows consumption (the wave's mean, rounded up): over 40 epochs the queue
+    settles below D and the refill produces what the steps consumed."""
     _need_gpu()
     from mgx import MgxEngine
     n = 4096
@@ -494,18 +497,23 @@ def test_refill_accounting():
     eng.reset()
     K, D = eng.refill_every, eng.ring_depth
     st = eng.stats()
-    assert st["queued"] == 2 * K * n and st["refill_launches"] == 1 and st["calls"] == 0
+    # to D, less the attempts abandoned on the way (each costs its lane one episode of the fill)
+    assert 0.97 * D * n <= st["queued"] <= D * n and st["refill_launches"] == 1 and st["calls"] == 0
     g = torch.Generator(device="cuda")
     g.manual_seed(5)
-    for epoch in range(3):
+    first = st
+    for epoch in range(40):
         prev = st
         for _ in range(K):
             eng.step(torch.randint(0, 7, (n,), device="cuda", generator=g, dtype=torch.int32))
         st = eng.stats()
         assert n * K <= st["queued"] <= n * D, (epoch, st)
         produced = (st["resets"] - prev["resets"]) + (st["queued"] - prev["queued"])
-        assert produced >= st["resets"] - prev["resets"] > 0, (epoch, st, prev)
+        assert produced >= 0 and st["resets"] - prev["resets"] > 0, (epoch, st, prev)
         assert st["refill_launches"] == 2 + epoch and st["calls"] == K * (epoch + 1)
+    consumed = st["resets"] - first["resets"]
+    produced = consumed + st["queued"] - first["queued"]
+    assert st["queued"] < D * n and produced > 0.9 * consumed, (st, first)
     eng.poll_error()
 
 
