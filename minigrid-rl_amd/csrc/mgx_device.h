@@ -220,11 +220,15 @@ __device__ __forceinline__ void pcg_seed(Pcg &p, uint64_t seed) {
 // slots, bit 5 of every slot a zero guard): 5x denser than the words, and a SWAR
 // compare tests ten candidate words at once (see randbelow).
 constexpr int MT_FIELDS = 10;       // words per packed group
-constexpr int MT_WG = 16;           // groups per lane-private LDS window (160 words)
-#ifndef MGX_MT_TOPUP
-#define MGX_MT_TOPUP 4      // window top-up when a lane has fewer than this many groups left (0: off)
-#endif
-constexpr int WIN_STRIDE = 34;      // dwords per lane window row: 8-B aligned, 2-way banked for b64
+// Groups per lane-private LDS window: 8 (80 words, about one episode's draws) for S <= 8, where the
+// refill wave's LDS (13 KB) then fits four to a CU beside four rollout workgroups; 16 for larger grids
+// (their LDS budget is set by the grids; the window reloads half as often).
+template <int NW>
+__host__ __device__ constexpr int mt_wg() { return NW == 1 ? 8 : 16; }
+constexpr int MT_WG_MAX = 16;
+template <int NW>   // dwords per lane window row: 8-B aligned, 2-way banked for b64
+__host__ __device__ constexpr int win_stride() { return 2 * mt_wg<NW>() + 2; }
+__host__ __device__ constexpr int win_stride_of(int nw) { return nw == 1 ? win_stride<1>() : win_stride<2>(); }
 constexpr uint64_t MT_REP = 0x041041041041041ull;   // 1 in every 6-bit slot of ten
 constexpr uint64_t MT_LOW60 = (1ull << 60) - 1ull;
 constexpr int MAX_OBJS = 32;     // objs list capacity bound; the list is sized per config (KParams.obj_cap)
@@ -277,7 +281,7 @@ struct Gen {
     const uint64_t *table; // packed MT19937 field groups (global ring of rmask+1 groups + mirror pad)
     uint64_t rmask;        // ring slots - 1 (a power of two): group g lives in slot g & rmask
     uint64_t tlo, thi;     // groups [tlo, thi) of the stream are in the ring (mgx_mt_slide_kernel)
-    uint64_t *win;         // LDS window: packed groups [gbase, gbase + MT_WG)
+    uint64_t *win;         // LDS window: packed groups [gbase, gbase + mt_wg<NW>())
     uint64_t gbase;        // first group in the window
     uint64_t cur, astart;  // word cursor; first word of the current reset attempt
     uint64_t ga, gb, gc;   // packed groups g, g+1 (ready), g+2 (LDS read in flight), g = cur / 10
@@ -342,11 +346,13 @@ __device__ __forceinline__ void put(Gen<NW> &G, int x, int y, uint8_t code) {   
 // Out of line: it is the cold path of every draw site (inlined at each of them it
 // made the generator ~2k instructions larger).
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
-constexpr int MT_PAD = MT_WG + 4;   // mirror pad groups after the ring (a window may start in its last slot)
+constexpr int MT_PAD = MT_WG_MAX + 4;   // mirror pad groups after the ring (a window may start in its last slot)
+template <int WG>
 __device__ __noinline__ void mt_refill_cold(const uint64_t *__restrict__ table, uint64_t slot, lds_u64 *win) {
     const uint4 *src = reinterpret_cast<const uint4 *>(table + slot);
+    static_assert(WG % 8 == 0 && WG <= MT_WG_MAX, "window loads go in fours of 16 B");
 #pragma unroll
-    for (int h = 0; h < MT_WG / 8; h++) {            // 4 x (4 loads in flight, then 8 LDS stores)
+    for (int h = 0; h < WG / 8; h++) {            // (4 loads in flight, then 8 LDS stores) per 8 groups
         const uint4 v0 = src[4 * h], v1 = src[4 * h + 1], v2 = src[4 * h + 2], v3 = src[4 * h + 3];
         lds_u64 *d = win + 8 * h;
         d[0] = (uint64_t)v0.x | ((uint64_t)v0.y << 32); d[1] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
@@ -357,12 +363,13 @@ __device__ __noinline__ void mt_refill_cold(const uint64_t *__restrict__ table, 
 }
 template <int NW>
 __device__ __forceinline__ uint64_t win_group(Gen<NW> &G, uint64_t g) {
+    constexpr int MT_WG = mt_wg<NW>();
     uint64_t off = g - G.gbase;
     if (off >= MT_WG) {
         GCOUNT(G, 23);
         // groups outside [tlo, thi) are not (or no longer) in the ring: MGX_DEVERR_MT_TABLE
         if (g < G.tlo || g + MT_WG > G.thi) G.err |= 1u;
-        mt_refill_cold(G.table, g & G.rmask, (lds_u64 *)G.win);
+        mt_refill_cold<MT_WG>(G.table, g & G.rmask, (lds_u64 *)G.win);
         G.gbase = g;
         off = 0;
     }
@@ -376,12 +383,13 @@ __device__ __forceinline__ uint64_t div10(uint64_t v) { return __umul64hi(v, 0xC
 template <int NW>
 __device__ __forceinline__ void mt_topup(Gen<NW> &G) {
 #if MGX_MT_TOPUP
+    constexpr int MT_WG = mt_wg<NW>();
     const uint64_t g = div10(G.cur);
     const int64_t used = (int64_t)(g - G.gbase);              // < 0 right after a look-ahead refill
     if (__ballot(used >= MT_WG - MGX_MT_TOPUP)) {
         if (used >= MT_WG / 2 && g >= G.tlo && g + MT_WG <= G.thi) {
             GCOUNT(G, 25);
-            mt_refill_cold(G.table, g & G.rmask, (lds_u64 *)G.win);
+            mt_refill_cold<MT_WG>(G.table, g & G.rmask, (lds_u64 *)G.win);
             G.gbase = g;
         }
     }
@@ -535,9 +543,14 @@ __device__ __forceinline__ bool occupied(const Gen<NW> &G, int b) {
 constexpr uint32_t OBJ_KEYFLAG = 1u << 24;
 template <int NW>
 __device__ __forceinline__ void add_obj(Gen<NW> &G, int t, int cname, int x, int y, uint32_t flags = 0) {
-    if (G.nobjs >= MAX_OBJS) { G.err |= 8u; return; }
-    G.objs[G.nobjs++] = (uint32_t)t | ((uint32_t)(cname & 15) << 4) | ((uint32_t)x << 8) | ((uint32_t)y << 16) | flags;
-    G.tmask |= 1u << t;
+    // branchless flags: with `if (full) { err |= 8; return; } ... tmask |= bit` the compiler sinks the
+    // two ORs into one through a select of &err / &tmask, which puts both fields on the stack
+    // (scratch loads with a full vmcnt wait in every placement)
+    const bool full = G.nobjs >= MAX_OBJS;
+    G.err |= full ? 8u : 0u;
+    G.tmask |= full ? 0u : 1u << t;
+    if (!full)
+        G.objs[G.nobjs++] = (uint32_t)t | ((uint32_t)(cname & 15) << 4) | ((uint32_t)x << 8) | ((uint32_t)y << 16) | flags;
 }
 
 // MiniGridEnv.place_obj position draw over the whole grid (PCG64): rejects occupied
@@ -1198,23 +1211,28 @@ __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
         place_obstacles(G);
         if (G.abort) return;
     }
-    R.range = 0;
+    // the mission's target as locals, R written once (per-branch stores to R's fields were merged
+    // through pointer selects, which put R on the stack)
+    uint32_t tx = NONE8, ty = NONE8, ta = NONE8, mid = CMD_GOTOGOAL;
+    uint64_t range = 0;
     if (EXT && cmd == 3) {                                        // 'drop'
-        R.tx = R.ty = NONE8; R.ta = A_DROP; R.mission_id = MID_DROP;
+        ta = A_DROP; mid = MID_DROP;
     } else if (EXT && cmd == 4) {                                 // 'move <dir>'
         const int d = pcg_integers(G.pcg, 0, 4);                  // np_random.choice(self.msn_directions)
-        R.range = move_range(G, d);
-        R.tx = R.ty = NONE8; R.ta = NONE8; R.mission_id = (uint8_t)(MID_MOVE + d);
+        range = move_range(G, d);
+        mid = MID_MOVE + d;
     } else if (cmd == 0) {                                               // 'go to' (np_random.integers)
         int i = 0;
+        uint32_t bad = 0;
         for (uint32_t it = 0;; ++it) {
-            if (it > PCG_LOOP_LIMIT) { G.err |= 4u; break; }
+            if (it > PCG_LOOP_LIMIT) { bad = 4u; break; }
             i = pcg_integers(G.pcg, 0, G.nobjs);
             if ((G.objs[i] & 15) != T_GOAL) break;
         }
+        G.err |= bad;
         const uint32_t o = G.objs[i];
-        R.tx = (uint8_t)(o >> 8); R.ty = (uint8_t)(o >> 16); R.ta = A_DONE;
-        R.mission_id = (uint8_t)(CMD_GOTO | (((o >> 4) & 15) << 2) | (type_slot(o & 15) << 5));
+        tx = (o >> 8) & 0xFF; ty = (o >> 16) & 0xFF; ta = A_DONE;
+        mid = CMD_GOTO | (((o >> 4) & 15) << 2) | (type_slot(o & 15) << 5);
     } else if (cmd == 1 || cmd == 2) {                            // 'toggle' / 'pick up' (random.choice)
         const uint32_t want = cmd == 1 ? (1u << T_BOX) | (1u << T_DOOR) : (1u << T_BOX) | (1u << T_KEY) | (1u << T_BALL);
         if (!(G.tmask & want)) { live_lock(G); return; }     // no such object: the reference loops forever
@@ -1225,17 +1243,15 @@ __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
             if ((want >> (G.objs[i] & 15)) & 1) break;
         }
         const uint32_t o = G.objs[i];
-        R.tx = (uint8_t)(o >> 8); R.ty = (uint8_t)(o >> 16);
-        R.ta = cmd == 1 ? A_TOGGLE : A_PICKUP;
-        R.mission_id = (uint8_t)((cmd == 1 ? CMD_TOGGLE : CMD_PICKUP) | (((o >> 4) & 15) << 2) |
-                                 (type_slot(o & 15) << 5));
+        tx = (o >> 8) & 0xFF; ty = (o >> 16) & 0xFF;
+        ta = cmd == 1 ? A_TOGGLE : A_PICKUP;
+        mid = (cmd == 1 ? CMD_TOGGLE : CMD_PICKUP) | (((o >> 4) & 15) << 2) | (type_slot(o & 15) << 5);
     } else {                                                      // 'go to goal'
-        R.tx = R.ty = NONE8;
         for (int k = 0; k < G.nobjs; k++)
-            if ((G.objs[k] & 15) == T_GOAL) { R.tx = (uint8_t)(G.objs[k] >> 8); R.ty = (uint8_t)(G.objs[k] >> 16); break; }
-        R.ta = NONE8;
-        R.mission_id = CMD_GOTOGOAL;
+            if ((G.objs[k] & 15) == T_GOAL) { tx = (G.objs[k] >> 8) & 0xFF; ty = (G.objs[k] >> 16) & 0xFF; break; }
     }
+    R.tx = (uint8_t)tx; R.ty = (uint8_t)ty; R.ta = (uint8_t)ta; R.mission_id = (uint8_t)mid;
+    R.range = range;
 }
 
 // MiniGridEnv.reset with the engine's live-lock retry policy.

@@ -77,7 +77,7 @@ constexpr long long MT_HOST_FILL = 1ll << 20;             // words the host gene
 // workgroup waited ~50 us for a whole CU behind the fused rollout, and the refill waited behind it)
 constexpr int SLIDE_THREADS = 256, SLIDE_ENVS = 16 * SLIDE_THREADS;
 // LDS bytes per resetting lane: MT window + objs list (obj_stride words, see mgx_create)
-__host__ __device__ constexpr int scratch_per_env(int obj_stride) { return WIN_STRIDE * 4 + obj_stride * 4; }
+__host__ __device__ constexpr int scratch_per_env(int obj_stride, int nw) { return win_stride_of(nw) * 4 + obj_stride * 4; }
 
 struct KParams {
     EnvState *state;
@@ -285,9 +285,10 @@ __device__ __forceinline__ void load_gen(Gen<NW> &G, const KParams &p, int64_t e
     G.tlo = p.mtc->lo;              // uniform: scalar loads; the slider runs between kernels, never during
     G.thi = p.mtc->hi;
     // lane >= 0: workgroup LDS layout [64 windows][64 objs lists]; lane < 0: one env's private block
-    G.win = reinterpret_cast<uint64_t *>(scratch + (lane >= 0 ? lane * (WIN_STRIDE * 4) : 0));
-    G.objs = reinterpret_cast<uint32_t *>(scratch + (lane >= 0 ? BLOCK_ENVS * (WIN_STRIDE * 4) + lane * (p.obj_stride * 4)
-                                                               : WIN_STRIDE * 4));
+    constexpr int WS = win_stride<NW>();
+    G.win = reinterpret_cast<uint64_t *>(scratch + (lane >= 0 ? lane * (WS * 4) : 0));
+    G.objs = reinterpret_cast<uint32_t *>(scratch + (lane >= 0 ? BLOCK_ENVS * (WS * 4) + lane * (p.obj_stride * 4)
+                                                               : WS * 4));
     G.llw = p.llw;
     G.err = 0;
     G.problem = p.problem;
@@ -1121,9 +1122,13 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
 // one's stores drain under another's step logic and render.
 //   waves 0-3  as mgx_step_kernel<., true>: wave 0 = one lane per env (env_step), then all four
 //              render 4 threads per env and copy their 16 rows out
-//   wave 4     LDS-DMA only (never waits on a store): actions of step t+1; for an env that popped at
-//              step t-1, its ring episode after next.  Every env keeps its next TWO ring episodes
-//              staged (buffer = ring position & 1), so a pop never waits.
+//   wave 4     LDS-DMA only: actions of step t+1; for an env that popped at step t-1, its ring
+//              episode after next, and the popped episode's RNG snapshot -> cur_rng (a step late:
+//              only the MT slider reads it during the launch, and an older cursor is a lower bound).
+//              Every env keeps its next TWO ring episodes staged (buffer = ring position & 1), so a
+//              pop never waits.
+// LDS: 4 workgroups + 4 refill waves per CU at S = 8 (26 + 13 KB each): the refill runs
+// beside the whole launch instead of waiting for its workgroups to retire.
 // Outputs of step t go to row t of [K][N] arrays; the env state, ring head and grids are written
 // back once, at the end.  The refill may run concurrently (it reads ring_head once, at its start:
 // a stale head only under-estimates its free slots); the K steps lie within one refill epoch, whose
@@ -1148,8 +1153,9 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     uint8_t *s_grid = smem + CSTK;                                     // current grids (chunk-major, cm_off)
     uint8_t *s_pg = s_grid + GB;                                       // [2] staged ring episodes' grids
     uint4 *s_ph = reinterpret_cast<uint4 *>(s_pg + 2 * GB);            // [2][64] their headers
-    uint4 *s_pr = s_ph + 2 * BLOCK_ENVS;                               // [2][2][64] their RNG snapshots
-    int32_t *s_act = reinterpret_cast<int32_t *>(s_pr + 4 * BLOCK_ENVS);   // [2][64] actions
+    int32_t *s_act = reinterpret_cast<int32_t *>(s_ph + 2 * BLOCK_ENVS);   // [2][64] actions
+    unsigned long long *s_mr = reinterpret_cast<unsigned long long *>(s_act + 2 * BLOCK_ENVS);
+                                                                       // [64] 'move' target_range (has_move only)
     __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params of the frame written (post-step view or
                                                  // the popped episode's first)
     __shared__ uint32_t s_rpt[BLOCK_ENVS];       // post-step view of a finished episode (terminal row)
@@ -1162,7 +1168,6 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     // per CU instead of 4)
     __shared__ uint4 s_st[BLOCK_ENVS];           // EnvState
     __shared__ uint8_t s_head[BLOCK_ENVS], s_pub[BLOCK_ENVS];
-    __shared__ unsigned long long s_mr[BLOCK_ENVS];   // 'move' target_range (problems mov / full)
     __shared__ unsigned long long s_cnt[2];      // resets, abandoned attempts
     __shared__ uint32_t s_err;
 
@@ -1178,7 +1183,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         s_st[lane] = reinterpret_cast<const uint4 *>(p.state)[e0 + lc];
         s_head[lane] = p.ring_head[e0 + lc];
         s_pub[lane] = p.ring_pub[e0 + lc];
-        s_mr[lane] = p.range_cur[p.has_move ? e0 + lc : 0];
+        if (p.has_move) s_mr[lane] = p.range_cur[e0 + lc];
         s_nh[1][lane] = 0xFF;
         if (lane < 2) s_cnt[lane] = 0;
         if (lane == 0) s_err = 0;
@@ -1188,22 +1193,25 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         for (int c = tid >> 6; c < GSQ; c += BLOCK_THREADS / 64)
             __builtin_amdgcn_global_load_lds(src + c, s_grid + c * (BLOCK_ENVS * 16), 16, 0, 0);
     }
-    // stage ring episode h of env e (this lane's) into buffer h & 1: header, RNG snapshot, grid
+    // stage ring episode h of env e (this lane's) into buffer h & 1: header, grid
     auto stage = [&](uint8_t h) {
         const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + (h & (D - 1));   // 32-bit offsets: fewer VGPRs
-        const uint4 *hs = p.ring_hdr + 3 * slot, *rs = p.ring_rng + 2 * slot;
+        const uint4 *hs = p.ring_hdr + 3 * slot;
         const uint4 *gs = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
         if (h & 1) {                                 // LDS-DMA destinations must be wave-uniform
             __builtin_amdgcn_global_load_lds(hs, s_ph + BLOCK_ENVS, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(rs, s_pr + 2 * BLOCK_ENVS, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(rs + 1, s_pr + 3 * BLOCK_ENVS, 16, 0, 0);
             for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + GB + c * (BLOCK_ENVS * 16), 16, 0, 0);
         } else {
             __builtin_amdgcn_global_load_lds(hs, s_ph, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(rs, s_pr, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(rs + 1, s_pr + BLOCK_ENVS, 16, 0, 0);
             for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + c * (BLOCK_ENVS * 16), 16, 0, 0);
         }
+    };
+    // cur_rng of an env that popped ring position h (its RNG snapshot; plain loads + stores)
+    auto rng_out = [&](uint8_t h) {
+        const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + (h & (D - 1));
+        const uint4 r0 = p.ring_rng[2 * slot], r1 = p.ring_rng[2 * slot + 1];
+        p.cur_rng[2 * (e0 + lane)] = r0;
+        p.cur_rng[2 * (e0 + lane) + 1] = r1;
     };
     if (dmaw && lane < ne) {
         __builtin_amdgcn_global_load_lds(actions + e0 + lane, s_act, 4, 0, 0);
@@ -1231,6 +1239,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                                                      4, 0, 0);
                 const uint8_t nh = s_nh[tb ^ 1][lanev];
                 if (nh != 0xFF && (uint8_t)(s_pub[lanev] - nh) > 1) stage((uint8_t)(nh + 1));
+                if (nh != 0xFF) rng_out((uint8_t)(nh - 1));
             }
         } else if (wave0) {
             // ---- the step: one lanev per env
@@ -1267,8 +1276,6 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                     // SubprocVecEnv auto-reset: the staged ring episode (header, RNG snapshot, grid)
                     popb = rhead & 1;
                     const uint4 h = s_ph[popb * BLOCK_ENVS + lanev];
-                    p.cur_rng[2 * e] = s_pr[(2 * popb) * BLOCK_ENVS + lanev];
-                    p.cur_rng[2 * e + 1] = s_pr[(2 * popb + 1) * BLOCK_ENVS + lanev];
                     if (p.has_move) s_mr[lanev] = p.ring_range[e * (uint32_t)D + (rhead & (D - 1))];
                     mid = (uint8_t)(h.y >> 16);
                     st.ax = (uint8_t)(h.x & 0xFF); st.ay = (uint8_t)((h.x >> 8) & 0xFF); st.dir = (uint8_t)((h.x >> 16) & 0xFF);
@@ -1363,7 +1370,12 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         if (dmaw) __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
     }
-    // ---- write back: state and ring head (wave 0), every grid, counters
+    // ---- write back: state and ring head (wave 0), every grid, counters; the DMA wave: cur_rng of
+    // the envs that popped at the last step
+    if (dmaw && lane < ne && K > 0) {
+        const uint8_t nh = s_nh[(K - 1) & 1][lane];
+        if (nh != 0xFF) rng_out((uint8_t)(nh - 1));
+    }
     if (wave0 && lane < ne) {
         reinterpret_cast<uint4 *>(p.state)[e0 + lane] = s_st[lane];
         p.ring_head[e0 + lane] = s_head[lane];
@@ -1581,6 +1593,8 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         atomicAdd(&p.counters[26], __builtin_amdgcn_s_memtime() - rc0);   // wave clocks
         atomicAdd(&p.counters[27], (unsigned long long)rc_iters);          // attempt rounds (busiest lane)
         atomicAdd(&p.counters[28], 1ull);                                  // waves
+        atomicAdd(&p.counters[8 + min(rc_iters, 15)], 1ull);               // waves by attempt rounds
+        atomicMax(&p.counters[29], __builtin_amdgcn_s_memtime() - rc0);   // slowest wave
     }
 #endif
     if (tid == 0) {
@@ -2401,7 +2415,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.obj_cap = std::min(MAX_OBJS, cfg->problem == MGX_PROBLEM_MULTI ? 9 + 2 * cfg->num_objects
                                    : (cfg->problem == MGX_PROBLEM_FULL ? 24 : cfg->num_objects) + 1);
     p.obj_stride = p.obj_cap | 1;
-    const int scratch = BLOCK_ENVS * scratch_per_env(p.obj_stride);
+    const int nw_ = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);   // generator variant (h->nw below)
+    const int scratch = BLOCK_ENVS * scratch_per_env(p.obj_stride, nw_);
     p.stk_lds = (std::max(BLOCK_ENVS * IMG, scratch) + 15) & ~15;   // reset kernel: stack area doubles as scratch
     p.grid_lds = (BLOCK_ENVS * (GS + 4) + 15) & ~15;
     p.fast_roll = cfg->n_stack == 4;
@@ -2470,9 +2485,11 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
                           + (size_t)BLOCK_ENVS * 3 * 16;                                     // + popped header, RNG snapshot
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
-    // fused rollout: frame rows + current grids + two staged ring episodes (grid, header, RNG) + actions
+    // fused rollout: frame rows + current grids + two staged ring episodes (grid, header) + actions
+    // [+ 'move' target ranges]
     h->lds_rollout = (size_t)((BLOCK_ENVS * FROW + 15) & ~15) + (size_t)BLOCK_ENVS * 3 * GS +
-                     (size_t)BLOCK_ENVS * 6 * 16 + (size_t)2 * BLOCK_ENVS * 4;
+                     (size_t)BLOCK_ENVS * 2 * 16 + (size_t)2 * BLOCK_ENVS * 4 +
+                     ((cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL) ? (size_t)BLOCK_ENVS * 8 : 0);
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
     h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
@@ -2484,7 +2501,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     MGX_SET_LDS1((K<1, false>), bytes); MGX_SET_LDS1((K<2, false>), bytes); MGX_SET_LDS1((K<4, false>), bytes); \
     MGX_SET_LDS1((K<1, true>), bytes); MGX_SET_LDS1((K<2, true>), bytes); MGX_SET_LDS1((K<4, true>), bytes)
     MGX_SET_LDS(mgx_reset_kernel, h->lds_reset);
-    h->lds_refill = (size_t)((64 * (GS + 4) + 15) & ~15) + (size_t)64 * scratch_per_env(p.obj_stride);
+    h->lds_refill = (size_t)((64 * (GS + 4) + 15) & ~15) + (size_t)64 * scratch_per_env(p.obj_stride, h->nw);
     MGX_SET_LDS(mgx_refill_kernel, h->lds_refill);
     MGX_SET_LDS1(mgx_refill_multi_kernel<1>, h->lds_refill); MGX_SET_LDS1(mgx_refill_multi_kernel<2>, h->lds_refill);
     MGX_SET_LDS1(mgx_refill_multi_kernel<4>, h->lds_refill);

@@ -27,6 +27,8 @@ for n in [int(v) for v in os.environ.get("NS", "1 8 64 65536").split()]:
     waves, rounds, clocks = c1[28] - c0[28], c1[27] - c0[27], c1[26] - c0[26]
     print(json.dumps(dict(n=n, waves=waves, rounds_per_wave_launch=rounds / waves,
                           clocks_per_round=clocks / max(rounds, 1),
+                          clocks_per_wave_launch=clocks / waves, max_wave_clocks=c1[29],
+                          rounds_histogram={r: c1[8 + r] - c0[8 + r] for r in range(16) if c1[8 + r] - c0[8 + r]},
                           episodes_per_env_launch=(s1["resets"] - s0["resets"]) / n /
                           max(1, s1["refill_launches"] - s0["refill_launches"]))), flush=True)
     e.close()
