@@ -879,23 +879,24 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     uint64_t reps = 0;                       // bit y*S of every row y (S <= 8): room masks by multiply
     if (NW == 1)
         for (int i = 0; i < S; i++) reps |= 1ull << (i * S);
-    int r = 0, phase = 0, kleft = 0, kx = -1, ky = -1;
-    bool fin = (MGX_GEN_SKIP & 1) != 0;
-    if (fin) return;
+    // The task sequence as one 64-bit set, consumed lowest bit first: room r owns bits 16r..16r+15,
+    // bit 0 of a room = key A, bit 1 = key B, bits 2.. = its objects (<= 9, num_objects <= 18).
+    // Advancing is `todo &= todo - 1` (a per-lane walk over rooms / phases was a divergent loop).
+    uint64_t todo = 0;
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++)
+        todo |= (uint64_t)(((keymask >> (2 * rr)) & 3u) | ((((1u << ((npack >> (8 * rr)) & 0xFF)) - 1u) & 0x3FFFu) << 2))
+                << (16 * rr);
+    if (MGX_GEN_SKIP & 1) return;
+    int kx = -1, ky = -1;                    // this room's key A (key B avoids it)
 #pragma unroll 1
-    for (int it = 0; it < 12; it++) {            // advance to the first task (bounded)
-        if (phase == 0) { if ((keymask >> (2 * r)) & 1) break; phase = 1; }
-        if (phase == 1) { if ((keymask >> (2 * r + 1)) & 1) break; phase = 2; kleft = (npack >> (8 * r)) & 0xFF; }
-        if (kleft > 0) break;
-        if (++r >= nr) { fin = true; break; }
-        phase = 0;
-    }
-#pragma unroll 1
-    while (!fin) {
+    while (todo) {
         GCOUNT(G, 20);
         GSTAMP(G, 19);                                           // (commit + task advance of the previous)
         if (!(MGX_GEN_SKIP & 16)) mt_topup(G);
         GSTAMP(G, 16);                                           // MT window top-up
+        const int slot = (int)__builtin_ctzll(todo);
+        const int r = slot >> 4, phase = min(slot & 15, 2);     // 0 key A, 1 key B, 2 object
         int x0, x1, y0, y1;
         room_rect(nr, r, mid, S, x0, x1, y0, y1);
         const bool is_key = phase < 2;
@@ -906,7 +907,7 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
             const uint32_t di = dinfo >> (8 * ((kspec >> (4 * r + 2 * phase)) & 3));
             cname = di & 7;
             kib = (di >> 4) & 1;
-            if (phase == 1) { ox = kx; oy = ky; }
+            if (phase == 1 && ((keymask >> (2 * r)) & 1)) { ox = kx; oy = ky; }   // key A came just before
         } else {
             if (oc == 0) { G.err |= 8u; break; }
             const int b = (MGX_GEN_SKIP & 32) ? __ffs(oc) - 1 : mask_choice(G, oc);
@@ -957,26 +958,13 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
             if (G.abort) return;
         }
         GSTAMP(G, 18);                                           // inner rejection loop
-        // commit the placement, then advance to the next task
+        // commit the placement, then the next task
         const int cidx = cn2idx(cname);
         const int t = is_key ? (kib ? T_BOX : T_KEY) : ot;
         put(G, x, y, mk_code(t, cidx, (is_key && kib) ? 1 : 0));
         add_obj(G, t, cname, x, y, is_key ? OBJ_KEYFLAG : 0u);
-        if (is_key) {
-            if (phase == 0) { kx = x; ky = y; }
-            phase++;
-            if (phase == 2) kleft = (npack >> (8 * r)) & 0xFF;
-        } else {
-            kleft--;
-        }
-#pragma unroll 1
-        for (int k2 = 0; k2 < 12; k2++) {
-            if (phase == 1) { if ((keymask >> (2 * r + 1)) & 1) break; phase = 2; kleft = (npack >> (8 * r)) & 0xFF; }
-            if (phase == 2 && kleft > 0) break;
-            if (phase == 0) { if ((keymask >> (2 * r)) & 1) break; phase = 1; continue; }
-            if (++r >= nr) { fin = true; break; }
-            phase = 0; kx = -1; ky = -1;
-        }
+        if (phase == 0) { kx = x; ky = y; }
+        todo &= todo - 1;
     }
     GSTAMP(G, 14);                                               // keys + objects, room by room
 }
