@@ -2196,7 +2196,8 @@ struct mgx_handle {
     bool refill_multi;      // problem 'multi' without EXT features refills with mgx_refill_multi_kernel
                             // (env MGX_REFILL_GENERIC=1: the all-problems kernel, for A/B checks)
     hipStream_t side;       // refill stream
-    hipEvent_t ev_fork, ev_done;
+    hipEvent_t ev_fork, ev_done, ev_slide;
+    bool slide_in_flight;   // the MT slide after the last forked refill may still run (ev_slide)
     void *allocs[17];
     uint32_t *scene_dev;    // mgx_scene's record (inside allocs[15], inline mode only)
 };
@@ -2295,6 +2296,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->refill_every = h->cfg.refill_every;
     h->calls = 0;
     h->in_flight = false;
+    h->slide_in_flight = false;
     {
         const char *sv = std::getenv("MGX_SERIAL_REFILL");
         h->serial_refill = sv && sv[0] == '1';
@@ -2513,6 +2515,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         hipError_t e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_slide, hipEventDisableTiming);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "side stream / events"));
     }
     (void)hipSetDevice(prev);
@@ -2531,6 +2534,7 @@ mgx_status mgx_destroy(mgx_handle *h) {
     }
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     if (h->ev_done) (void)hipEventDestroy(h->ev_done);
+    if (h->ev_slide) (void)hipEventDestroy(h->ev_slide);
     for (void *&p : h->allocs) if (p) { (void)hipFree(p); p = nullptr; }
     (void)hipSetDevice(prev);
     delete h;
@@ -2557,13 +2561,12 @@ static mgx_status launch_slide(mgx_handle *h, void *stream) {
     return MGX_OK;
 }
 
-static mgx_status launch_refill(mgx_handle *h, void *stream) {
+// One refill launch, then the MT slide for the NEXT one (round 3: the slide used to precede its refill
+// and held it back ~27 us per epoch beside a rollout; after it, it runs in the shadow of the join).
+// `done`: event recorded between the two (the epoch join waits for the refill only).
+static mgx_status launch_refill(mgx_handle *h, void *stream, hipEvent_t done = nullptr) {
     if (h->kp.D == 0) return MGX_OK;
     h->refill_launches++;
-    {   // (mgx_reset's fill: from where the reset kernel left the cursors; D episodes ahead)
-        mgx_status ss = launch_slide(h, stream);
-        if (ss != MGX_OK) return ss;
-    }
     const int64_t nblk = (h->kp.n + 63) / 64;
     if (h->refill_multi && !h->ext && h->kp.problem == MGX_PROBLEM_MULTI) {
         const dim3 g((unsigned)nblk), b(64);
@@ -2574,13 +2577,21 @@ static mgx_status launch_refill(mgx_handle *h, void *stream) {
         MGX_GEN_LAUNCH(mgx_refill_kernel, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp);
     }
     HIP_TRY(hipGetLastError());
-    return MGX_OK;
+    if (done) HIP_TRY(hipEventRecord(done, (hipStream_t)stream));
+    // the next refill's window of the MT stream: generated ahead of the cursors this one left
+    return launch_slide(h, stream);
 }
 
-static mgx_status join_refill(mgx_handle *h, void *stream) {
+// full: also the MT slide that follows the refill (mgx_join, mgx_reset: nothing of the handle's left
+// running on the side stream); the epoch fork waits for the refill alone.
+static mgx_status join_refill(mgx_handle *h, void *stream, bool full = true) {
     if (h->in_flight) {
         HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, h->ev_done, 0));
         h->in_flight = false;
+    }
+    if (full && h->slide_in_flight) {
+        HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, h->ev_slide, 0));
+        h->slide_in_flight = false;
     }
     return MGX_OK;
 }
@@ -2591,17 +2602,18 @@ static mgx_status join_refill(mgx_handle *h, void *stream) {
 static mgx_status fork_refill(mgx_handle *h, void *stream) {
     // the previous epoch's refill is joined here, not at that epoch's last step: work the caller
     // enqueues between epochs (GAE, the policy forward) runs beside the refill's tail
-    mgx_status js = join_refill(h, stream);
+    mgx_status js = join_refill(h, stream, false);
     if (js != MGX_OK) return js;
     HIP_TRY(hipMemcpyAsync(h->kp.ring_pub, h->kp.ring_tail, (size_t)h->kp.n, hipMemcpyDeviceToDevice,
                            (hipStream_t)stream));
     if (h->serial_refill) return launch_refill(h, stream);
     HIP_TRY(hipEventRecord(h->ev_fork, (hipStream_t)stream));
-    HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
-    mgx_status s = launch_refill(h, h->side);
+    HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));      // (the side stream is in order: the
+    mgx_status s = launch_refill(h, h->side, h->ev_done);     //  previous slide precedes this refill)
     if (s != MGX_OK) return s;
-    HIP_TRY(hipEventRecord(h->ev_done, h->side));
+    HIP_TRY(hipEventRecord(h->ev_slide, h->side));
     h->in_flight = true;
+    h->slide_in_flight = true;
     return MGX_OK;
 }
 
