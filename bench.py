@@ -3,11 +3,15 @@
 Workload (one "step" = one vectorised step of the whole per-GPU batch:
 PlaygroundEnv.step + gen_obs + the two wrappers + SubprocVecEnv auto-reset, the
 new observation written into the rollout buffer in the compact layout -- one
-148-B row + mission id per env (`mgx_step_compact`; the collector's stacked
-VecFrameStack(4) input is rebuilt from rows by `mgx_gather`, bit-exact with the
-materialised stacks, tests/test_compact.py).  At N=1 the same workload with the
-materialised SB3 stacks (`mgx_step`: VecTransposeImage + VecFrameStack roll per
-step, the MgxVecEnv drop-in) is timed too and reported as `sb3_layout`):
+148-B row + mission id per env; the collector's stacked VecFrameStack(4) input
+is rebuilt from rows by `mgx_gather`, bit-exact with the materialised stacks,
+tests/test_compact.py).  The actions of this random-action rollout are known up
+front, so the headline runs each refill epoch's steps in one launch
+(`mgx_rollout_compact`, bit-exact with per-step calls, tests/test_rollout.py).
+At N=1 the same workload is also timed with one launch per step
+(`mgx_step_compact`: the path a policy in the loop takes) as `compact_layout`
+and with the materialised SB3 stacks (`mgx_step`: VecTransposeImage +
+VecFrameStack roll per step, the MgxVecEnv drop-in) as `sb3_layout`):
   multi / mission 5 ('go to goal', GTG) / 8x8 / num_objects 4 / 65,536 envs per
   GPU, uniform random actions on {0..6} (pre-generated on device for all
   warmup+timed steps, so inputs are resident in HBM), seed 42, env global
@@ -19,13 +23,15 @@ episodes produced vs consumed), and every `horizon` steps it runs GAE over the
 rewards/dones the steps wrote (mgx_gae_dones, synthetic values) and, for N>1,
 the one all-reduce of the (sum A, sum A^2, n) advantage statistics (RCCL).
 
-Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel
-(mgx_step_kernel) with SURVEY.md §8(d)'s algorithmic bytes
-  B_alg = 334*steps + (3*S^2 + 208)*resets     (per launch: one step of all N envs)
-divided by its average launch duration, measured live with HIP events on the
-launch stream around each run of consecutive mgx_step calls that neither fork nor join a refill epoch
-(so the event pair brackets only mgx_step_kernel launches, which still run
-concurrently with that epoch's refill, as in the timed region);
+Prints ONE JSON line (rank 0).  `roofline` prices the kernel that runs the steps
+(mgx_rollout_kernel in the fused headline, mgx_step_kernel per step) with
+SURVEY.md §8(d)'s algorithmic bytes
+  B_alg = 334*steps + (3*S^2 + 208)*resets     (per step: one step of all N envs)
+divided by its average duration per step, measured live with HIP events on the
+launch stream: fused, one event pair around each epoch's launch (the epoch's refill
+beside it); per step, around each run of consecutive mgx_step calls that neither
+fork nor join a refill epoch (those launches still run concurrently with that
+epoch's refill, as in the timed region);
 `traffic` is the rocprofv3 PMC figure committed under profiles/.  `gae` times
 mgx_gae_dones alone at the horizon and at T=1024 (17 B per element).
 `cpu_baseline` times the C port of the env (oracle/) on this host's cores.
@@ -88,12 +94,13 @@ def parse():
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
     ap.add_argument("--eval-episodes", type=int, default=100,
                     help="ppo: deterministic evaluate_policy episodes after the timed iterations (0: none)")
-    ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layout")
+    ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layouts")
     ap.add_argument("--layout", default=None, choices=["compact", "sb3", "fused"],
-                    help="observation storage: compact rows + mgx_gather (mgx_step_compact, one launch per "
-                         "step; the default of both workloads), the same rows from one launch per refill epoch "
-                         "(fused: mgx_rollout_compact, actions known up front) or the materialised SB3 stacks "
-                         "(mgx_step, the VecEnv drop-in's)")
+                    help="observation storage: compact rows + mgx_gather from one launch per refill epoch "
+                         "(fused: mgx_rollout_compact, actions known up front; the rollout default when the "
+                         "timed steps are whole epochs), the same rows from one launch per step "
+                         "(mgx_step_compact; the ppo default) or the materialised SB3 stacks (mgx_step, the "
+                         "VecEnv drop-in's)")
     args = ap.parse_args()
     presets = {2: dict(mission="5", size=8, n_envs=65536), 4: dict(mission="None", size=8, n_envs=32768),
                5: dict(mission="1", size=16, n_envs=131072)}
@@ -108,7 +115,9 @@ def parse():
     if ppo and args.horizon is None:
         args.horizon = 16
     if args.layout is None:
-        args.layout = "compact"
+        # rollout: the fused launch per refill epoch (the actions of a random-action rollout are known
+        # up front); it needs the timed steps to be whole epochs (pick_epoch), else one launch per step
+        args.layout = "compact" if ppo or pick_epoch(args.steps, args.ring_depth or 128) is None else "fused"
     return args
 
 
@@ -681,11 +690,13 @@ def main():
         return main_ppo(args, world, rank, local, dev)
     out = measure_rollout(args, args.layout, world, rank, dev)
     if world == 1 and args.both_layouts:
-        # the other observation layout on the same workload, reported beside the headline
-        other = "sb3" if args.layout == "compact" else "compact"
-        torch.cuda.empty_cache()
-        o2 = measure_rollout(args, other, world, rank, dev)
-        out[other + "_layout"] = {k: o2[k] for k in ("value", "ms_per_step", "roofline", "window")}
+        # the other observation layouts on the same workload, reported beside the headline: one launch
+        # per step (compact rows: the path a policy in the loop takes) and the materialised SB3 stacks
+        # (the MgxVecEnv drop-in's)
+        for other in [l for l in ("compact", "sb3") if l != args.layout]:
+            torch.cuda.empty_cache()
+            o2 = measure_rollout(args, other, world, rank, dev)
+            out[other + "_layout"] = {k: o2[k] for k in ("value", "ms_per_step", "roofline", "window")}
     if rank == 0:
         out["ranks_seen"] = ranks_seen
         out["dist_backend"] = dist.get_backend() if world > 1 else None

@@ -2303,7 +2303,10 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         const char *st = std::getenv("MGX_STEP_PRIO");
         h->kp.step_prio = st ? std::atoi(st) : 0;
         const char *rp = std::getenv("MGX_REFILL_PRIO");
-        h->kp.refill_prio = rp ? std::atoi(rp) : 0;
+        // refill waves at issue priority 2 over co-resident step / rollout waves: the refill sets the
+        // pipeline beside the fused rollout (+3-7 % at config 2, +4 % at config 4; per-step layouts
+        // and config 5 within +-0.5 %, tools/gpu_prio3.sh / gpu_prio4.sh)
+        h->kp.refill_prio = rp ? std::atoi(rp) : 2;
         const char *pm = std::getenv("MGX_REFILL_MEAN");
         h->kp.prod_mean = pm ? std::atoi(pm) : 2;
         const char *rg = std::getenv("MGX_REFILL_GENERIC");
