@@ -652,6 +652,9 @@ def measure_rollout(args, layout, world, rank, dev):
                          "probe_launches": len(probe_us),
                          "step_pipeline_us": float(gpu_ms) * 1e3 / K,
                          "alg_bytes_per_launch": b_alg, "resets_per_launch": resets_per_launch,
+                         # the same duration priced with the PMC bytes instead of B_alg: the fused kernel
+                         # moves less than B_alg (grids and env state stay in LDS for the whole epoch)
+                         "traffic_frac": (traffic / per_launch_s / 1e9 / PEAK_HBM_GBPS) if traffic else None,
                          "stack_bytes_per_launch": stack_bytes,
                          "achieved_incl_stack": (b_alg + stack_bytes) / per_launch_s / 1e9},
             "gae": {"horizon": gae_h, "T1024": gae_1k},
