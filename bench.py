@@ -80,7 +80,7 @@ def parse():
     ap.add_argument("--probe", type=int, default=256, help="eager steps timed per launch for the roofline")
     ap.add_argument("--workload", default="rollout", choices=["rollout", "ppo"])
     ap.add_argument("--refill-every", type=int, default=0, help="steps per refill epoch (0 = engine default, D/4)")
-    ap.add_argument("--min-warmup", type=int, default=2048,
+    ap.add_argument("--min-warmup", type=int, default=256,
                     help="rollout: the warm-up is at least this many steps (whole refill epochs)")
     ap.add_argument("--refill-cap", type=int, default=0, help="extra episodes per env per epoch (0 = engine default)")
     ap.add_argument("--ring-depth", type=int, default=0, help="episode ring depth (0 = engine default)")
@@ -406,10 +406,10 @@ def measure_rollout(args, layout, world, rank, dev):
                     refill_every=E or 0, refill_cap=args.refill_cap, ring_depth=args.ring_depth)
     E = eng.refill_every
     H = pick_horizon(K, E if aligned else None, args.horizon or 0)
-    # warm-up: whole refill epochs, and at least 2,048 steps -- the rings start at 2E episodes and
-    # fill towards D at (cap - consumption) per env per epoch, ~1.3 episodes per 32 steps; a
-    # shorter warm-up would time that fill-up (the refill producing more than the steps consume),
-    # not the steady state, where production = consumption (`window` reports both)
+    # warm-up: whole refill epochs, and at least --min-warmup (256) steps.  mgx_reset fills every ring
+    # to D, so production follows consumption from the first epoch; but every env starts its first
+    # episode at step 0, and the reset rate (what the refill pays for) settles only after a few
+    # max_steps (64 at S = 8): a window right after the reset would see fewer resets than steady state
     W = -(-max(args.warmup, args.min_warmup, 1) // E) * E
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -617,10 +617,10 @@ def measure_rollout(args, layout, world, rank, dev):
             "steps": K,
             "warmup": W + (K if graphs else 0),          # + one untimed replay of the graphs
             "warmup_requested": args.warmup,
-            "warmup_note": "warm-up raised to >= 2,048 steps in whole refill epochs (+ one untimed replay of "
-                           "each graph): the episode rings fill towards their depth for ~1,500 steps after a "
-                           "reset, and the timed window pays for every episode it consumes (`window`), so a "
-                           "shorter warm-up would time the fill-up instead of the steady state",
+            "warmup_note": "warm-up raised to >= %d steps in whole refill epochs (+ one untimed replay of "
+                           "each graph): every env starts its first episode at the reset, and the reset rate "
+                           "the timed window pays for (`window`) settles only after a few max_steps; a window "
+                           "right after the reset would see fewer resets than steady state" % args.min_warmup,
             "ms_per_step": wall_max * 1e3 / K,
             "higher_is_better": True,
             "scaling": "weak",
