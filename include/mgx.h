@@ -84,9 +84,10 @@ typedef struct mgx_config {
     int32_t livelock_words;    /* 0 -> MGX_LIVELOCK_WORDS */
     int32_t terminal_mode;     /* mgx_terminal_mode */
     int32_t mission_int64;     /* 1: mission tokens int64 (TokenizeVocabWrapper dtype), 0: uint8 */
-    int32_t refill_cap;        /* episodes an env may pre-generate per refill epoch beyond what keeps the
-                                  ring from running dry (0 -> max(2, round(0.19 * refill_every)), i.e. 6
-                                  at the default epoch; < 0 -> fill the ring) */
+    int32_t refill_cap;        /* > 0 (0 -> max(2, round(0.19 * refill_every))): a refill epoch's production
+                                  per env follows the consumption of its 64-env wave since the previous
+                                  refill (the mean, rounded up), beyond what keeps the ring from running
+                                  dry; < 0 -> fill the ring every epoch.  mgx_reset fills every ring */
     int64_t mt_table_words;    /* 0 -> default (2^24): MT19937 output words the device keeps (rounded up to a
                                   power of two of 10-word groups, >= 5,120).  The stream is extended on the
                                   device as cursors advance -- no lifetime limit; only the spread between
@@ -139,7 +140,8 @@ mgx_status mgx_destroy(mgx_handle *h);
  * calls follow SB3: seeded (PCG64 only) if mgx_set_seed was called since the
  * last reset, else unseeded; both streams continue from each env's current
  * episode, and mission_done / the stored reward persist.
- * `livelock_dev` (optional i32 [N]). */
+ * It also pre-generates ring_depth episodes per env (on `stream`; ~6.5 ms at
+ * 65,536 envs, S = 8).  `livelock_dev` (optional i32 [N]). */
 mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, void *stream);
 
 /* VecEnv.seed(seed) (SB3): the NEXT mgx_reset seeds env i's PCG64 with

@@ -1161,7 +1161,8 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     __shared__ uint32_t s_rpt[BLOCK_ENVS];       // post-step view of a finished episode (terminal row)
     __shared__ uint8_t s_term[BLOCK_ENVS];       // terminal row written this step
     __shared__ uint8_t s_popb[BLOCK_ENVS];       // staged buffer popped this step (0xFF: none)
-    __shared__ uint8_t s_nh[2][BLOCK_ENVS];      // [step & 1] new ring head of an env that popped (0xFF: none)
+    // [step & 1] new ring head of an env that popped; 0xFFFF: none (u16: every u8 head value is a real one)
+    __shared__ uint16_t s_nh[2][BLOCK_ENVS];
     __shared__ unsigned long long s_tmask;
     // per-env state between steps lives in LDS, not registers: a loop-carried value would stay live
     // through the render, where the register pressure peaks (in registers: 128 VGPRs, 3 workgroups
@@ -1184,7 +1185,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         s_head[lane] = p.ring_head[e0 + lc];
         s_pub[lane] = p.ring_pub[e0 + lc];
         if (p.has_move) s_mr[lane] = p.range_cur[e0 + lc];
-        s_nh[1][lane] = 0xFF;
+        s_nh[1][lane] = 0xFFFF;
         if (lane < 2) s_cnt[lane] = 0;
         if (lane == 0) s_err = 0;
     }
@@ -1237,14 +1238,15 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 if (t + 1 < K)
                     __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lanev, s_act + (tb ^ 1) * BLOCK_ENVS,
                                                      4, 0, 0);
-                const uint8_t nh = s_nh[tb ^ 1][lanev];
-                if (nh != 0xFF && (uint8_t)(s_pub[lanev] - nh) > 1) stage((uint8_t)(nh + 1));
-                if (nh != 0xFF) rng_out((uint8_t)(nh - 1));
+                const uint16_t nh = s_nh[tb ^ 1][lanev];
+                if (nh != 0xFFFF && (uint8_t)(s_pub[lanev] - nh) > 1) stage((uint8_t)(nh + 1));
+                if (nh != 0xFFFF) rng_out((uint8_t)(nh - 1));
             }
         } else if (wave0) {
             // ---- the step: one lanev per env
             bool tw = false;
-            uint8_t popb = 0xFF, nh = 0xFF;
+            uint8_t popb = 0xFF;
+            uint16_t nh = 0xFFFF;
             if (lanev < ne) {
                 const uint32_t e = (uint32_t)(e0 + lanev), oi = (uint32_t)t * (uint32_t)N + e;   // N * K < 2^32
                 EnvState st;
@@ -1373,8 +1375,8 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     // ---- write back: state and ring head (wave 0), every grid, counters; the DMA wave: cur_rng of
     // the envs that popped at the last step
     if (dmaw && lane < ne && K > 0) {
-        const uint8_t nh = s_nh[(K - 1) & 1][lane];
-        if (nh != 0xFF) rng_out((uint8_t)(nh - 1));
+        const uint16_t nh = s_nh[(K - 1) & 1][lane];
+        if (nh != 0xFFFF) rng_out((uint8_t)(nh - 1));
     }
     if (wave0 && lane < ne) {
         reinterpret_cast<uint4 *>(p.state)[e0 + lane] = s_st[lane];

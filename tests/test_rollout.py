@@ -88,6 +88,40 @@ def test_rollout_equals_per_step(case, chunks):
     assert sb["queued"] >= E * n, sb
 
 
+def test_rollout_ring_positions_wrap():
+    """Ring positions are u8 counters (mod 256): over 640 steps with 'done' on 3 of 4 actions every
+    env pops > 256 episodes, so every head passes 255 -> 0 (and takes the value 255, which the fused
+    kernel's 'no pop' marker must not alias).  Fused chunks equal per-step calls bit for bit."""
+    _need_gpu()
+    from mgx.compact import CompactBuffer
+    n, E, T = 512, 32, 64
+    ref, fus = _engines(dict(problem="multi", mission=5, size=8), n, refill_every=E)
+    br, bf = CompactBuffer(ref, T), CompactBuffer(fus, T)
+    ref.reset(); fus.reset()
+    br.observe(0); bf.observe(0)
+    g = torch.Generator(device=ref.device)
+    g.manual_seed(77)
+    for rollout in range(10):
+        if rollout:
+            br.carry_over(); bf.carry_over()
+        acts = torch.randint(0, 7, (T, n), device=ref.device, generator=g, dtype=torch.int32)
+        acts = torch.where(torch.rand((T, n), device=ref.device, generator=g) < 0.75, 6, acts).to(torch.int32)
+        for t in range(0, T, E):
+            bf.rollout(t, acts[t:t + E].contiguous())
+            for j in range(E):
+                br.step(t + j, acts[t + j])
+        for name in ("rows", "mids", "starts", "rewards", "terminated", "truncated"):
+            assert torch.equal(getattr(br, name), getattr(bf, name)), (rollout, name)
+        assert torch.equal(br.terminal_rows, bf.terminal_rows), rollout
+    ref.poll_error()
+    fus.poll_error()
+    a, b = ref.dump_state(), fus.dump_state()
+    for k in a:
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k
+    sa, sb = ref.stats(), fus.stats()
+    assert sa["resets"] == sb["resets"] > 300 * n, (sa, sb)
+
+
 @pytest.mark.parametrize("problem,mission,size,n,T", [("multi", 5, 8, 65536, 64), ("multi", 1, 16, 131072, 32)],
                          ids=["cfg2_65536", "cfg5_131072"])
 def test_rollout_full_size_matches_oracle(problem, mission, size, n, T):
