@@ -117,7 +117,7 @@ def parse():
     if args.layout is None:
         # rollout: the fused launch per refill epoch (the actions of a random-action rollout are known
         # up front); it needs the timed steps to be whole epochs (pick_epoch), else one launch per step
-        args.layout = "compact" if ppo or pick_epoch(args.steps, args.ring_depth or 128) is None else "fused"
+        args.layout = "compact" if ppo or pick_epoch(args.steps, args.ring_depth or 256) is None else "fused"
     return args
 
 
@@ -340,13 +340,13 @@ def _ppo_success(pol, env_kw, episodes, dev):
             "seconds": round(time.perf_counter() - t0, 3)}
 
 
-def pick_epoch(K, D=128):
+def pick_epoch(K, D=256):
     """Refill epoch E (mgx refill_every) so that the K timed steps are whole epochs: the largest
-    divisor of K in [8, D/4] (at D/2 the ring invariant 2E <= D makes every epoch refill the rings
-    to full, so each wave runs as many rounds as its busiest lane consumed; at <= D/4 the
+    divisor of K in [8, min(64, D/4)] (at D/2 the ring invariant 2E <= D makes every epoch refill the
+    rings to full, so each wave runs as many rounds as its busiest lane consumed; at <= D/4 the
     production cap bounds them); K < 8 -> E = K.  None when K has no such divisor (then E = D/4
     and the timed region ends with mgx_join, paying for the whole last epoch's refill)."""
-    for E in range(min(32, D // 4), 7, -1):
+    for E in range(min(64, D // 4), 7, -1):
         if K % E == 0:
             return E
     return K if K < 8 else None
@@ -398,7 +398,7 @@ def measure_rollout(args, layout, world, rank, dev):
     n = args.n_envs
     mission = None if args.mission == "None" else int(args.mission)
     K = args.steps
-    D = args.ring_depth or 128
+    D = args.ring_depth or 256
     E = args.refill_every or pick_epoch(K, D)
     aligned = E is not None and K % E == 0
     eng = MgxEngine(problem=args.problem, mission=mission, size=args.size, n_envs=n, seed=42,

@@ -88,12 +88,13 @@ typedef struct mgx_config {
                                   per env follows the consumption of its 64-env wave since the previous
                                   refill (the mean, rounded up), beyond what keeps the ring from running
                                   dry; < 0 -> fill the ring every epoch.  mgx_reset fills every ring */
-    int64_t mt_table_words;    /* 0 -> default (2^24): MT19937 output words the device keeps (rounded up to a
+    int64_t mt_table_words;    /* 0 -> default (2^26): MT19937 output words the device keeps (rounded up to a
                                   power of two of 10-word groups, >= 5,120).  The stream is extended on the
                                   device as cursors advance -- no lifetime limit; only the spread between
                                   the oldest live cursor and the newest must stay below it */
-    int32_t ring_depth;        /* pre-generated episodes per env (0 -> 128; rounded up to a power of two
-                                  <= 128; -1 = no ring: every auto-reset generated inline) */
+    int32_t ring_depth;        /* pre-generated episodes per env (0 -> 256; rounded up to a power of two
+                                  <= 4096, ring positions are mod 2^16; -1 = no ring: every auto-reset
+                                  generated inline) */
     int32_t refill_every;      /* steps per refill epoch K (0 -> ring_depth/4; clamped to <= ring_depth/2:
                                   each epoch keeps >= K queued, and a step pops <= 1 episode) */
     double percent_obstacles;  /* `env.percent_obstacles` (single.yaml:28: 0.05); used when obstacles */

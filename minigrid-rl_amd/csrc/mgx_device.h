@@ -155,6 +155,10 @@ __device__ __forceinline__ int pcg_integers(Pcg &p, int lo, int hi) {
     uint32_t rng = (uint32_t)(hi - 1 - lo);
     if (rng == 0) return lo;
     uint32_t rng_excl = rng + 1u;
+    // a power-of-two range (every goal / agent / direction draw: integers(0, S) with S = 8 or 16,
+    // integers(0, 4)): m = x << k, so the low word is never below the threshold (0) and the draw is
+    // x's top k bits -- the same value without the 32 x 32 multiply
+    if (rng_excl != 0u && (rng_excl & rng) == 0u) return lo + (int)(pcg_next32(p) >> (32 - __builtin_ctz(rng_excl)));
     uint64_t m = (uint64_t)pcg_next32(p) * rng_excl;
     uint32_t left = (uint32_t)m;
     if (left < rng_excl) {
@@ -285,6 +289,7 @@ struct Gen {
     uint64_t gbase;        // first group in the window
     uint64_t cur, astart;  // word cursor; first word of the current reset attempt
     uint64_t ga, gb, gc;   // packed groups g, g+1 (ready), g+2 (LDS read in flight), g = cur / 10
+    uint64_t gi;           // g (kept with the queue: no 64-bit division per group rotation)
     int go;                // cur % 10
     uint32_t llw;
     bool abort;
@@ -384,7 +389,7 @@ template <int NW>
 __device__ __forceinline__ void mt_topup(Gen<NW> &G) {
 #if MGX_MT_TOPUP
     constexpr int MT_WG = mt_wg<NW>();
-    const uint64_t g = div10(G.cur);
+    const uint64_t g = G.gi;                                  // = cur / 10 (the register queue's group)
     const int64_t used = (int64_t)(g - G.gbase);              // < 0 right after a look-ahead refill
     if (__ballot(used >= MT_WG - MGX_MT_TOPUP)) {
         if (used >= MT_WG / 2 && g >= G.tlo && g + MT_WG <= G.thi) {
@@ -400,6 +405,7 @@ template <int NW>
 __device__ __forceinline__ void mt_sync(Gen<NW> &G) {
     const uint64_t g = div10(G.cur);
     G.go = (int)(G.cur - g * MT_FIELDS);
+    G.gi = g;
     G.ga = win_group(G, g);
     G.gb = win_group(G, g + 1);
     G.gc = win_group(G, g + 2);
@@ -449,7 +455,8 @@ __device__ __forceinline__ int randbelow_c(Gen<NW> &G, const RbConst K) {
             G.go -= MT_FIELDS;
             G.ga = G.gb;
             G.gb = G.gc;
-            G.gc = win_group(G, div10(G.cur) + 2);
+            G.gi++;
+            G.gc = win_group(G, G.gi + 2);
         }
         if (j < MT_FIELDS) return r;
     }
@@ -463,7 +470,8 @@ __device__ __forceinline__ void mt_advance(Gen<NW> &G, int m) {
         G.go -= MT_FIELDS;
         G.ga = G.gb;
         G.gb = G.gc;
-        G.gc = win_group(G, div10(G.cur) + 2);
+        G.gi++;
+        G.gc = win_group(G, G.gi + 2);
     }
 }
 // The reference's rejection loop `while True: x = randint(x0, x1); y = randint(y0, y1);

@@ -41,6 +41,9 @@ namespace {
 #define MGX_DIAG_SKIP 0     // diagnostics only: skip store classes (1 pass-1, 2 pass-2, 4 missions, 16 grids)
 #endif
 constexpr int BLOCK_ENVS = 64;
+typedef uint16_t rpos_t;                    // episode ring positions (mod 2^16)
+constexpr int MGX_MAX_RING = 4096;          // ring depth bound (a power of two, far below 2^16)
+constexpr uint32_t NO_POP = 0xFFFFFFFFu;    // mgx_rollout_kernel: no pop this step
 constexpr int MGX_NCOUNTERS = 32;          // [0..3] unused (per-workgroup slots), [4..7] step stamps, [8..] generator stamps
 constexpr int BLOCK_THREADS = 256;
 constexpr int FRAME = 147;                 // 3 x 7 x 7
@@ -67,6 +70,9 @@ struct MtCtl {
     unsigned int done;               // workgroups of the running pass that have reduced
     unsigned int pad;
     uint32_t st[624];                // MT19937 state at word hi * 10 (every output of it consumed)
+    // refill production ceiling (mgx_refill_kernel): the episodes every env popped between the last two
+    // refill launches, summed by the slide that follows the last one (running sum, result)
+    unsigned long long cons_run, cons_last;
 };
 constexpr int MT_SB_WORDS = 3120;                         // lcm(624, 10): five MT blocks = 312 whole groups
 constexpr int MT_SB_GROUPS = MT_SB_WORDS / MT_FIELDS;
@@ -109,11 +115,15 @@ struct KParams {
                             //           then the mission's 32 tokens (the step kernel's pop needs no lookup)
     uint4 *ring_rng;        // [N][D][2] RNG snapshot after that episode's generation
     uint4 *cur_rng;         // [N][2]   RNG snapshot after the current episode's generation
-    // SPSC ring indices (mod 256; D is a power of two <= 128):
-    uint8_t *ring_head;     // [N] consumer (step kernel) position
-    uint8_t *ring_tail;     // [N] producer (refill kernel) position
-    uint8_t *ring_pub;      // [N] ring_tail as of the last join: the step kernel pops below it
-    uint8_t *ring_seen;     // [N] ring_head as the last refill read it (its consumption estimate)
+    // SPSC ring indices (rpos_t, mod 2^16; D is a power of two <= MGX_MAX_RING):
+    rpos_t *ring_head;      // [N] consumer (step kernel) position
+    rpos_t *ring_tail;      // [N] producer (refill kernel) position
+    rpos_t *ring_pub;       // [N] ring_pubn as of the epoch's first per-step call: mgx_step_kernel pops below it
+    rpos_t *ring_pubn;      // [N] ring_tail as the last COMPLETED refill left it, copied by the slide that follows
+                            // it on the refill stream (a refill still running may have written ring_tail before
+                            // its episodes reached another XCD's view; a completed one has released them):
+                            // mgx_rollout_kernel pops below it, no copy on the steps' stream
+    rpos_t *ring_seen;      // [N] ring_head as the last refill read it (its consumption estimate)
     uint32_t *fix_list;     // [N] envs whose ring was empty at their reset (mgx_fixup_kernel)
     uint32_t *fix_count;    // list length; fix_done: workgroups of the fixup kernel that finished
     uint32_t *fix_done;
@@ -128,6 +138,8 @@ struct KParams {
     int refill_prio;        // s_setprio of the refill's waves (env MGX_REFILL_PRIO, 0..3)
     int prod_mean;          // refill production cap per wave (env MGX_REFILL_MEAN): 0 fixed `cap`,
                             // 1 the wave's mean deficit (<= cap), 2 its mean consumption, rounded up
+    int cap_max;            // ceiling of that per-wave cap (env MGX_REFILL_CAPMAX): > 0 fixed, 0 none,
+                            // -1 (default) the previous launch's mean consumption per env + 1/4, rounded up
     uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
                             //        generation (mgx_scene regenerates it), else null
 };
@@ -404,7 +416,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
         if (p.has_move) p.range_cur[e] = R.range;
         store_rng(G, p, e);
         rng_snapshot(G, p.cur_rng + 2 * e);
-        p.ring_head[e] = 0; p.ring_tail[e] = 0; p.ring_pub[e] = 0;   // empty ring (mgx_refill_kernel fills)
+        p.ring_head[e] = 0; p.ring_tail[e] = 0; p.ring_pub[e] = 0; p.ring_pubn[e] = 0;   // empty ring
         p.ring_seen[e] = 0;
         // stacked obs: zeros + first frame
         uint8_t *row = o.img + e * (int64_t)p.img_bytes;
@@ -620,7 +632,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     EnvState st;
     int a = 0;
     uint4 odir = make_uint4(0, 0, 0, 0);          // old direction stack (n_stack == 4: one uint4)
-    uint8_t rhead = 0, rpub = 0;                  // this env's ring position and published end
+    rpos_t rhead = 0, rpub = 0;                   // this env's ring position and published end
     uint64_t mrange = 0;                          // 'move' target_range (problems mov / full only)
     // (a) fast roll: the old image-stack dwords this lane's output quads need, into registers
     constexpr int DW = FRAME_DW4;                                                     // 147
@@ -702,7 +714,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // barrier without waiting: its latency runs under wave 0's step logic, and only the pop
     // (after the post-logic barrier, which wave 1 reaches once the DMA has landed) reads it.
     const bool spec = p.D > 0 && (a == A_FORWARD || a == A_DONE || st.step_count + 1 >= S * S) &&
-                      (uint8_t)(rpub - rhead) != 0;
+                      (rpos_t)(rpub - rhead) != 0;
     const bool wave1 = (tid >> 6) == 1;
     // Every phase-1 load of this wave has landed (register loads and LDS-DMA alike).  Saying
     // so explicitly matters: otherwise the waitcnt pass assumes a qa/qb load may be pending
@@ -773,7 +785,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             __builtin_amdgcn_s_waitcnt(0);
         }
         if (avail) {                                 // the pop itself follows the next barrier
-            new_head = (int)(uint8_t)(rhead + 1);   // published after a barrier, loads consumed
+            new_head = (int)(rpos_t)(rhead + 1);    // published after a barrier, loads consumed
             dirty = true;
             popped = true;
         } else if (done && p.D > 0) {
@@ -856,7 +868,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // ring heads: the popped slot is consumed (its DMA landed in phase 1), so the refill may
     // reuse it.  Every lane writes its head, changed or not: one 64-B store per block instead
     // of a byte store per popped env.
-    if (tid < ne && p.D > 0) p.ring_head[e0 + tid] = (uint8_t)(new_head >= 0 ? new_head : rhead);
+    if (tid < ne && p.D > 0) p.ring_head[e0 + tid] = (rpos_t)(new_head >= 0 ? new_head : rhead);
     // ---- phase 5 (issued here, before the render, so the stores drain under it): write back
     // the grids that changed (moves, pickups, resets; a popped env's new grid is in the staging
     // area, both chunk-major), at line granularity: grids smaller than a 128-B line are written
@@ -1161,14 +1173,14 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     __shared__ uint32_t s_rpt[BLOCK_ENVS];       // post-step view of a finished episode (terminal row)
     __shared__ uint8_t s_term[BLOCK_ENVS];       // terminal row written this step
     __shared__ uint8_t s_popb[BLOCK_ENVS];       // staged buffer popped this step (0xFF: none)
-    // [step & 1] new ring head of an env that popped; 0xFFFF: none (u16: every u8 head value is a real one)
-    __shared__ uint16_t s_nh[2][BLOCK_ENVS];
+    // [step & 1] new ring head of an env that popped; NO_POP: none (u32: every rpos_t value is a real one)
+    __shared__ uint32_t s_nh[2][BLOCK_ENVS];
     __shared__ unsigned long long s_tmask;
     // per-env state between steps lives in LDS, not registers: a loop-carried value would stay live
     // through the render, where the register pressure peaks (in registers: 128 VGPRs, 3 workgroups
     // per CU instead of 4)
     __shared__ uint4 s_st[BLOCK_ENVS];           // EnvState
-    __shared__ uint8_t s_head[BLOCK_ENVS], s_pub[BLOCK_ENVS];
+    __shared__ rpos_t s_head[BLOCK_ENVS], s_pub[BLOCK_ENVS];
     __shared__ unsigned long long s_cnt[2];      // resets, abandoned attempts
     __shared__ uint32_t s_err;
 
@@ -1183,9 +1195,8 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     if (wave0) {
         s_st[lane] = reinterpret_cast<const uint4 *>(p.state)[e0 + lc];
         s_head[lane] = p.ring_head[e0 + lc];
-        s_pub[lane] = p.ring_pub[e0 + lc];
         if (p.has_move) s_mr[lane] = p.range_cur[e0 + lc];
-        s_nh[1][lane] = 0xFFFF;
+        s_nh[1][lane] = NO_POP;
         if (lane < 2) s_cnt[lane] = 0;
         if (lane == 0) s_err = 0;
     }
@@ -1195,10 +1206,11 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             __builtin_amdgcn_global_load_lds(src + c, s_grid + c * (BLOCK_ENVS * 16), 16, 0, 0);
     }
     // stage ring episode h of env e (this lane's) into buffer h & 1: header, grid
-    auto stage = [&](uint8_t h) {
-        const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + (h & (D - 1));   // 32-bit offsets: fewer VGPRs
+    auto stage = [&](rpos_t h) {
+        const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + (h & (D - 1));   // N * D < 2^32
         const uint4 *hs = p.ring_hdr + 3 * slot;
-        const uint4 *gs = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
+        // the grid's byte offset is 64-bit: N * D * GS reaches 2^33 at config 5 (131,072 x 256 x 256)
+        const uint4 *gs = reinterpret_cast<const uint4 *>(p.ring_grid + (size_t)slot * (size_t)p.GS);
         if (h & 1) {                                 // LDS-DMA destinations must be wave-uniform
             __builtin_amdgcn_global_load_lds(hs, s_ph + BLOCK_ENVS, 16, 0, 0);
             for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + GB + c * (BLOCK_ENVS * 16), 16, 0, 0);
@@ -1208,7 +1220,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         }
     };
     // cur_rng of an env that popped ring position h (its RNG snapshot; plain loads + stores)
-    auto rng_out = [&](uint8_t h) {
+    auto rng_out = [&](rpos_t h) {
         const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + (h & (D - 1));
         const uint4 r0 = p.ring_rng[2 * slot], r1 = p.ring_rng[2 * slot + 1];
         p.cur_rng[2 * (e0 + lane)] = r0;
@@ -1216,10 +1228,15 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     };
     if (dmaw && lane < ne) {
         __builtin_amdgcn_global_load_lds(actions + e0 + lane, s_act, 4, 0, 0);
-        const uint8_t rhead = p.ring_head[e0 + lane], rpub = p.ring_pub[e0 + lane];
-        const int q = (uint8_t)(rpub - rhead);
+        // the end of the env's published episodes: ring_pubn, read ONCE (the slide after a refill running
+        // beside this launch may raise it meanwhile; every value it takes is a completed refill's), shared
+        // with the step wave through s_pub so that the staging and the pops agree
+        const rpos_t rhead = p.ring_head[e0 + lane];
+        const rpos_t rpub = *reinterpret_cast<volatile const rpos_t *>(p.ring_pubn + e0 + lane);
+        s_pub[lane] = rpub;
+        const int q = (rpos_t)(rpub - rhead);
         if (q > 0) stage(rhead);
-        if (q > 1) stage((uint8_t)(rhead + 1));
+        if (q > 1) stage((rpos_t)(rhead + 1));
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -1238,15 +1255,15 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 if (t + 1 < K)
                     __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lanev, s_act + (tb ^ 1) * BLOCK_ENVS,
                                                      4, 0, 0);
-                const uint16_t nh = s_nh[tb ^ 1][lanev];
-                if (nh != 0xFFFF && (uint8_t)(s_pub[lanev] - nh) > 1) stage((uint8_t)(nh + 1));
-                if (nh != 0xFFFF) rng_out((uint8_t)(nh - 1));
+                const uint32_t nh = s_nh[tb ^ 1][lanev];
+                if (nh != NO_POP && (rpos_t)(s_pub[lanev] - nh) > 1) stage((rpos_t)(nh + 1));
+                if (nh != NO_POP) rng_out((rpos_t)(nh - 1));
             }
         } else if (wave0) {
             // ---- the step: one lanev per env
             bool tw = false;
             uint8_t popb = 0xFF;
-            uint16_t nh = 0xFFFF;
+            uint32_t nh = NO_POP;
             if (lanev < ne) {
                 const uint32_t e = (uint32_t)(e0 + lanev), oi = (uint32_t)t * (uint32_t)N + e;   // N * K < 2^32
                 EnvState st;
@@ -1254,7 +1271,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                     const uint4 sv = s_st[lanev];
                     __builtin_memcpy(&st, &sv, sizeof st);
                 }
-                uint8_t rhead = s_head[lanev];
+                rpos_t rhead = s_head[lanev];
                 uint64_t mrange = p.has_move ? s_mr[lanev] : 0ull;
                 uint32_t err = 0;
                 int a = s_act[tb * BLOCK_ENVS + lanev];
@@ -1274,7 +1291,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 }
                 uint8_t mid = st.mission_id;
                 int lvl = 0;
-                if (r.done && (uint8_t)(s_pub[lanev] - rhead) != 0) {
+                if (r.done && (rpos_t)(s_pub[lanev] - rhead) != 0) {
                     // SubprocVecEnv auto-reset: the staged ring episode (header, RNG snapshot, grid)
                     popb = rhead & 1;
                     const uint4 h = s_ph[popb * BLOCK_ENVS + lanev];
@@ -1375,8 +1392,8 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     // ---- write back: state and ring head (wave 0), every grid, counters; the DMA wave: cur_rng of
     // the envs that popped at the last step
     if (dmaw && lane < ne && K > 0) {
-        const uint16_t nh = s_nh[(K - 1) & 1][lane];
-        if (nh != 0xFFFF) rng_out((uint8_t)(nh - 1));
+        const uint32_t nh = s_nh[(K - 1) & 1][lane];
+        if (nh != NO_POP) rng_out((rpos_t)(nh - 1));
     }
     if (wave0 && lane < ne) {
         reinterpret_cast<uint4 *>(p.state)[e0 + lane] = s_st[lane];
@@ -1490,13 +1507,13 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
 #endif
     // The step kernel may be popping this env's ring concurrently: `head` can be stale
     // (older, smaller), which only under-estimates the free slots.
-    uint8_t tail = 0;
+    rpos_t tail = 0;
     int level = 0, cons = 0;
     if (e < p.n) {
-        const uint8_t head = *reinterpret_cast<volatile const uint8_t *>(p.ring_head + e);
+        const rpos_t head = *reinterpret_cast<volatile const rpos_t *>(p.ring_head + e);
         tail = p.ring_tail[e];
-        level = (int)(uint8_t)(tail - head);
-        cons = (int)(uint8_t)(head - p.ring_seen[e]);    // episodes popped since the last refill read
+        level = (int)(rpos_t)(tail - head);
+        cons = (int)(rpos_t)(head - p.ring_seen[e]);     // episodes popped since the last refill read
         p.ring_seen[e] = head;
     }
     const int space = p.D - level, need = 2 * p.K - level;
@@ -1522,6 +1539,19 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         }
         cnt = max(cnt, 1);
         cap = by_cons ? (sum + cnt - 1) / cnt : min(cap, (2 * sum + cnt) / (2 * cnt));
+        if (p.cap_max > 0) cap = min(cap, p.cap_max);
+        if (p.cap_max < 0 && by_cons) {
+            // The launch lasts as long as its slowest wave, and a wave runs as many attempt rounds as
+            // its cap: a ceiling common to all waves keeps the few waves whose lanes popped more than
+            // the rest (one in ten would round up to 6 at config 2) from setting the launch.  Their
+            // lanes keep the difference as a deficit, which the ring depth absorbs and later epochs
+            // (every wave's consumption has the same mean) pay back.
+            const unsigned long long last = p.mtc->cons_last;      // wave-uniform (scalar load)
+            if (last) {
+                const unsigned long long n4 = 4ull * (unsigned long long)p.n;
+                cap = min(cap, max(1, (int)((4ull * last + (unsigned long long)p.n + n4 - 1ull) / n4)));
+            }
+        }
     }
     if (e < p.n) {
         // mgx_reset's fill: every ring to D (not just the invariant's 2K), so the epochs that follow
@@ -1577,7 +1607,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
                 tail++;
             }
             store_rng(G, p, e, (uint32_t)livelocks);
-            p.ring_tail[e] = tail;                 // published to the step kernel at the next join
+            p.ring_tail[e] = tail;                 // published by the slide that follows (ring_pubn)
             maxcur = G.cur;
             err = G.err;
         }
@@ -1599,12 +1629,15 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         atomicMax(&p.counters[29], __builtin_amdgcn_s_memtime() - rc0);   // slowest wave
     }
 #endif
+    // this wave's consumption since the last refill: mgx_mt_slide_kernel, which follows every refill, sums
+    // it over the waves into MtCtl.cons_last (the next launch's production ceiling)
+    int csum = e < p.n ? cons : 0;
+    for (int off = 32; off > 0; off >>= 1) csum += __shfl_xor(csum, off);
     if (tid == 0) {
-        if (maxcur) {
-            ulonglong4 b = p.blk[2 * p.nblk + blockIdx.x];
-            b.w = b.w > maxcur ? b.w : maxcur;
-            p.blk[2 * p.nblk + blockIdx.x] = b;
-        }
+        ulonglong4 b = p.blk[2 * p.nblk + blockIdx.x];
+        b.w = b.w > maxcur ? b.w : maxcur;
+        b.x = (unsigned long long)csum;
+        p.blk[2 * p.nblk + blockIdx.x] = b;
         if (err) atomicOr(p.err, err);
     }
 }
@@ -1713,6 +1746,7 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     for (int k = 0; k < SLIDE_ENVS / SLIDE_THREADS; k++) {
         const int64_t e = e0 + k * SLIDE_THREADS + tid;
         if (e < p.n) {
+            if (p.D > 0) p.ring_pubn[e] = p.ring_tail[e];   // the refill before this slide has completed
             const uint4 cr = p.cur_rng[2 * e + 1];
             unsigned long long v = (unsigned long long)cr.z | ((unsigned long long)cr.w << 32);
             if (p.start_rng) {
@@ -1726,10 +1760,17 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
             mx = w > mx ? w : mx;
         }
     }
+    // the refill waves' consumption (mgx_refill_kernel writes it in its workgroup stats): one per 64 envs
+    unsigned long long cs = 0;
+    if (tid < SLIDE_ENVS / 64) {
+        const int64_t b = e0 / 64 + tid;
+        if (b < p.nblk) cs = p.blk[2 * p.nblk + b].x;
+    }
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long o = __shfl_xor(mn, off), q = __shfl_xor(mx, off);
         mn = o < mn ? o : mn;
         mx = q > mx ? q : mx;
+        cs += __shfl_xor(cs, off);
     }
     if ((tid & 63) == 0) { s_red[tid >> 6] = mn; s_red2[tid >> 6] = mx; }
     __syncthreads();
@@ -1740,6 +1781,7 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
         }
         atomicMin(&c->span_min, mn);
         atomicMax(&c->span_max, mx);
+        if (cs) atomicAdd(&c->cons_run, cs);        // (wave 0 holds every block of this workgroup)
         __threadfence();
         s_nsb = atomicAdd(&c->done, 1u) == gridDim.x - 1 ? 1 : -1;   // last workgroup: pass 2
     }
@@ -1747,6 +1789,7 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     if (s_nsb < 0) return;
     if (tid == 0) {
         __threadfence();
+        c->cons_last = atomicExch(&c->cons_run, 0ull);   // the last refill's consumption, all envs
         const unsigned long long m = atomicExch(&c->span_min, ~0ull);   // every workgroup's extremes; reset
         const unsigned long long x = atomicExch(&c->span_max, 0ull);
         c->done = 0;
@@ -2193,13 +2236,13 @@ struct mgx_handle {
     uint64_t resets;        // mgx_reset calls since create
     uint64_t refill_launches;  // refill kernels enqueued since create (incl. the synchronous initial fills)
     bool seed_pending;      // mgx_set_seed called since the last reset
-    bool in_flight;         // a refill forked and not yet joined
+    bool in_flight;         // a refill (and the slide after it) forked and not yet joined
+    bool pub_stale;         // ring_pub not yet copied from ring_tail this epoch (mgx_step_kernel reads it)
     bool serial_refill;     // diagnostics (env MGX_SERIAL_REFILL=1): refill on the caller's stream
     bool refill_multi;      // problem 'multi' without EXT features refills with mgx_refill_multi_kernel
                             // (env MGX_REFILL_GENERIC=1: the all-problems kernel, for A/B checks)
     hipStream_t side;       // refill stream
-    hipEvent_t ev_fork, ev_done, ev_slide;
-    bool slide_in_flight;   // the MT slide after the last forked refill may still run (ev_slide)
+    hipEvent_t ev_fork, ev_done;
     void *allocs[17];
     uint32_t *scene_dev;    // mgx_scene's record (inside allocs[15], inline mode only)
 };
@@ -2282,12 +2325,15 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->cfg = *cfg;
     h->device = device;
     if (h->cfg.livelock_words <= 0) h->cfg.livelock_words = MGX_LIVELOCK_WORDS;
-    if (h->cfg.ring_depth == 0) h->cfg.ring_depth = 128;
+    // default depth 256 (round 3; 128 before): at refill epochs of D/4 = 64 steps the lanes' deficits
+    // (production follows the wave's mean consumption, capped at the grid's) stay far from the invariant's
+    // 2K, so need-driven attempt rounds do not set the launch
+    if (h->cfg.ring_depth == 0) h->cfg.ring_depth = 256;
     if (h->cfg.ring_depth < 0) {
         h->cfg.ring_depth = 0;                                   // ring disabled: every reset generated inline
     } else {
         int d = 2;
-        while (d < h->cfg.ring_depth && d < 128) d <<= 1;        // power of two (mod-256 ring indices)
+        while (d < h->cfg.ring_depth && d < MGX_MAX_RING) d <<= 1;   // power of two (mod-2^16 ring indices)
         h->cfg.ring_depth = d;
     }
     if (h->cfg.refill_every <= 0) h->cfg.refill_every = std::max(1, h->cfg.ring_depth / 4);
@@ -2298,7 +2344,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->refill_every = h->cfg.refill_every;
     h->calls = 0;
     h->in_flight = false;
-    h->slide_in_flight = false;
+    h->pub_stale = true;
     {
         const char *sv = std::getenv("MGX_SERIAL_REFILL");
         h->serial_refill = sv && sv[0] == '1';
@@ -2311,6 +2357,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         h->kp.refill_prio = rp ? std::atoi(rp) : 2;
         const char *pm = std::getenv("MGX_REFILL_MEAN");
         h->kp.prod_mean = pm ? std::atoi(pm) : 2;
+        const char *cm = std::getenv("MGX_REFILL_CAPMAX");
+        h->kp.cap_max = cm ? std::atoi(cm) : -1;
         const char *rg = std::getenv("MGX_REFILL_GENERIC");
         h->refill_multi = !(rg && rg[0] == '1');
     }
@@ -2340,12 +2388,12 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     }
     const int D = h->cfg.ring_depth;
     {
-        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 48, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 4 + 64};
+        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 48, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 5 * sizeof(rpos_t) + 64};
         for (int i = 0; i < 5; i++) {
             hipError_t e = hipMalloc(&h->allocs[7 + i], rs[i] ? rs[i] : 16);
             if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, std::string("hipMalloc ring: ") + hipGetErrorString(e)));
         }
-        hipError_t e = hipMemset(h->allocs[11], 0, (size_t)N * 4 + 64);
+        hipError_t e = hipMemset(h->allocs[11], 0, (size_t)N * 5 * sizeof(rpos_t) + 64);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset ring ctl"));
         e = hipMemset(h->allocs[10], 0, (size_t)N * 32);      // cursors read by the MT slider before any reset
         if (e == hipSuccess) e = hipMemset(h->allocs[3], 0, (size_t)N * 16);
@@ -2443,10 +2491,11 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.ring_hdr = (uint4 *)h->allocs[8];
     p.ring_rng = (uint4 *)h->allocs[9];
     p.cur_rng = (uint4 *)h->allocs[10];
-    p.ring_head = (uint8_t *)h->allocs[11];
+    p.ring_head = (rpos_t *)h->allocs[11];
     p.ring_tail = p.ring_head + N;
     p.ring_pub = p.ring_head + 2 * N;
     p.ring_seen = p.ring_head + 3 * N;
+    p.ring_pubn = p.ring_head + 4 * N;
     p.fix_list = (uint32_t *)h->allocs[12];
     p.fix_count = p.fix_list + N + 4;       // 16-B aligned tail of the same allocation
     p.fix_done = p.fix_list + N + 8;
@@ -2520,7 +2569,6 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         hipError_t e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_slide, hipEventDisableTiming);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "side stream / events"));
     }
     (void)hipSetDevice(prev);
@@ -2539,7 +2587,6 @@ mgx_status mgx_destroy(mgx_handle *h) {
     }
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     if (h->ev_done) (void)hipEventDestroy(h->ev_done);
-    if (h->ev_slide) (void)hipEventDestroy(h->ev_slide);
     for (void *&p : h->allocs) if (p) { (void)hipFree(p); p = nullptr; }
     (void)hipSetDevice(prev);
     delete h;
@@ -2567,8 +2614,7 @@ static mgx_status launch_slide(mgx_handle *h, void *stream) {
 }
 
 // One refill launch, then the MT slide for the NEXT one (round 3: the slide used to precede its refill
-// and held it back ~27 us per epoch beside a rollout; after it, it runs in the shadow of the join).
-// `done`: event recorded between the two (the epoch join waits for the refill only).
+// and held it back ~27 us per epoch beside a rollout).  `done`: event recorded after both.
 static mgx_status launch_refill(mgx_handle *h, void *stream, hipEvent_t done = nullptr) {
     if (h->kp.D == 0) return MGX_OK;
     h->refill_launches++;
@@ -2582,43 +2628,52 @@ static mgx_status launch_refill(mgx_handle *h, void *stream, hipEvent_t done = n
         MGX_GEN_LAUNCH(mgx_refill_kernel, dim3((unsigned)nblk), dim3(64), h->lds_refill, (hipStream_t)stream, h->kp);
     }
     HIP_TRY(hipGetLastError());
+    // the next refill's window of the MT stream: generated ahead of the cursors this one left; the
+    // slide also publishes this refill's tails (ring_pubn), so the epoch join (`done`) waits for it
+    mgx_status ss = launch_slide(h, stream);
+    if (ss != MGX_OK) return ss;
     if (done) HIP_TRY(hipEventRecord(done, (hipStream_t)stream));
-    // the next refill's window of the MT stream: generated ahead of the cursors this one left
-    return launch_slide(h, stream);
+    return MGX_OK;
 }
 
 // full: also the MT slide that follows the refill (mgx_join, mgx_reset: nothing of the handle's left
 // running on the side stream); the epoch fork waits for the refill alone.
-static mgx_status join_refill(mgx_handle *h, void *stream, bool full = true) {
+static mgx_status join_refill(mgx_handle *h, void *stream) {
     if (h->in_flight) {
         HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, h->ev_done, 0));
         h->in_flight = false;
     }
-    if (full && h->slide_in_flight) {
-        HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, h->ev_slide, 0));
-        h->slide_in_flight = false;
-    }
     return MGX_OK;
 }
 
-// Epoch start: publish the tails the last refill reached, then fork this epoch's
-// refill onto the side stream.  It writes only slots the step kernel cannot pop
-// before the next publish, and RNG state only the refill uses.
+// Epoch start: join the last refill (and the slide after it, which published its tails in ring_pubn),
+// then fork this epoch's refill onto the side stream.  It writes only slots the steps cannot pop before
+// the next publish, and RNG state only the refill uses.
 static mgx_status fork_refill(mgx_handle *h, void *stream) {
     // the previous epoch's refill is joined here, not at that epoch's last step: work the caller
-    // enqueues between epochs (GAE, the policy forward) runs beside the refill's tail
-    mgx_status js = join_refill(h, stream, false);
+    // enqueues between epochs (GAE, the policy forward) runs beside the refill's tail.  No copy on this
+    // stream: the fused rollout reads ring_pubn, the per-step calls copy it to ring_pub at their first
+    // call (publish_for_steps)
+    mgx_status js = join_refill(h, stream);
     if (js != MGX_OK) return js;
-    HIP_TRY(hipMemcpyAsync(h->kp.ring_pub, h->kp.ring_tail, (size_t)h->kp.n, hipMemcpyDeviceToDevice,
-                           (hipStream_t)stream));
+    h->pub_stale = true;
     if (h->serial_refill) return launch_refill(h, stream);
     HIP_TRY(hipEventRecord(h->ev_fork, (hipStream_t)stream));
-    HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));      // (the side stream is in order: the
-    mgx_status s = launch_refill(h, h->side, h->ev_done);     //  previous slide precedes this refill)
+    HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    mgx_status s = launch_refill(h, h->side, h->ev_done);
     if (s != MGX_OK) return s;
-    HIP_TRY(hipEventRecord(h->ev_slide, h->side));
     h->in_flight = true;
-    h->slide_in_flight = true;
+    return MGX_OK;
+}
+
+// mgx_step_kernel pops below ring_pub, which must not move within a launch (its waves read it
+// independently): a copy of ring_pubn made at the epoch's first per-step call (any byte it holds is a
+// completed refill's tail).
+static mgx_status publish_for_steps(mgx_handle *h, void *stream) {
+    if (!h->pub_stale) return MGX_OK;
+    HIP_TRY(hipMemcpyAsync(h->kp.ring_pub, h->kp.ring_pubn, (size_t)h->kp.n * sizeof(rpos_t), hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+    h->pub_stale = false;
     return MGX_OK;
 }
 
@@ -2708,6 +2763,10 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
         mgx_status fs = fork_refill(h, stream);
         if (fs != MGX_OK) return fs;
     }
+    if (h->kp.D > 0) {
+        mgx_status ps = publish_for_steps(h, stream);
+        if (ps != MGX_OK) return ps;
+    }
     if (action_bytes == 4)
         hipLaunchKernelGGL((mgx_step_kernel<int32_t, false>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
                            (hipStream_t)stream, h->kp, o, (const int32_t *)actions_dev);
@@ -2753,6 +2812,8 @@ mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_b
         mgx_status fs = fork_refill(h, stream);
         if (fs != MGX_OK) return fs;
     }
+    mgx_status ps = publish_for_steps(h, stream);
+    if (ps != MGX_OK) return ps;
     if (action_bytes == 4)
         hipLaunchKernelGGL((mgx_step_kernel<int32_t, true>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step_compact,
                            (hipStream_t)stream, h->kp, o, (const int32_t *)actions_dev);
@@ -2929,12 +2990,17 @@ mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]) {
     HIP_TRY(hipMemcpy(b.data(), h->kp.blk, b.size() * sizeof(ulonglong4), hipMemcpyDeviceToHost));
     uint64_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // blk sections: [0, nblk) step kernel (x steps, y resets), [nblk, 2 nblk) fixup, [2 nblk, 3 nblk)
-    // refill; z live-locks and w max MT cursor in every section
-    for (const ulonglong4 &v : b) { c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] = v.w > c[3] ? v.w : c[3]; }
-    if (h->kp.D > 0) {   // episodes queued in the rings: sum of (tail - head) mod 256
-        std::vector<uint8_t> ht((size_t)2 * h->kp.n);
-        HIP_TRY(hipMemcpy(ht.data(), h->kp.ring_head, ht.size(), hipMemcpyDeviceToHost));
-        for (int64_t i = 0; i < h->kp.n; i++) c[4] += (uint8_t)(ht[(size_t)(h->kp.n + i)] - ht[(size_t)i]);
+    // refill (x: that wave's consumption at its last launch, not a counter); z live-locks and w max MT cursor
+    // in every section
+    for (size_t i = 0; i < b.size(); i++) {
+        const ulonglong4 &v = b[i];
+        if (i < (size_t)2 * h->kp.nblk) c[0] += v.x;
+        c[1] += v.y; c[2] += v.z; c[3] = v.w > c[3] ? v.w : c[3];
+    }
+    if (h->kp.D > 0) {   // episodes queued in the rings: sum of (tail - head) mod 2^16
+        std::vector<rpos_t> ht((size_t)2 * h->kp.n);
+        HIP_TRY(hipMemcpy(ht.data(), h->kp.ring_head, ht.size() * sizeof(rpos_t), hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < h->kp.n; i++) c[4] += (rpos_t)(ht[(size_t)(h->kp.n + i)] - ht[(size_t)i]);
     }
     c[5] = h->refill_launches;
     c[6] = h->calls;

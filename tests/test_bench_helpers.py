@@ -9,14 +9,14 @@ import bench  # noqa: E402
 
 
 def test_pick_epoch():
-    assert bench.pick_epoch(2048) == 32          # D/4 at D = 128
+    assert bench.pick_epoch(2048) == 64          # D/4 at D = 256
     assert bench.pick_epoch(20) == 20            # the driver's --steps 20
-    assert bench.pick_epoch(96) == 32
+    assert bench.pick_epoch(96) == 48
     assert bench.pick_epoch(5) == 5              # K < 8: one epoch
-    assert bench.pick_epoch(67) is None          # prime > 32: joined partial epoch
+    assert bench.pick_epoch(67) is None          # prime > 64: joined partial epoch
     for K in (20, 64, 100, 2048, 4096):
         E = bench.pick_epoch(K)
-        assert K % E == 0 and 8 <= E <= 32
+        assert K % E == 0 and 8 <= E <= 64
 
 
 def test_pick_horizon():
