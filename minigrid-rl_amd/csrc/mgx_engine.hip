@@ -1241,8 +1241,17 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 
+#ifdef MGX_RSTAMPS
+    // diagnostics (-DMGX_RSTAMPS): wave 0's clocks per phase, summed over the steps -> counters[4..7]
+    unsigned long long rs_c[4] = {0, 0, 0, 0}, rs_t = 0;
+#define RSTAMP(k) do { if (tid == 0) { const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+                                       rs_c[(k) > 0 ? (k) - 1 : 0] += (k) > 0 ? _t - rs_t : 0ull; rs_t = _t; } } while (0)
+#else
+#define RSTAMP(k) do { } while (0)
+#endif
     for (int t = 0; t < K; t++) {
         const int tb = t & 1;
+        RSTAMP(0);
         // thread index through an opaque copy: lane- / env-derived addresses are then computed inside
         // each region of the step, instead of being hoisted out of the loop and kept live through all of
         // them (96 -> fewer VGPRs; the render's and the step logic's registers no longer add up)
@@ -1330,7 +1339,9 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             const unsigned long long tm = __ballot(tw);
             if (lanev == 0) s_tmask = tm;
         }
+        RSTAMP(1);                                     // step logic (wave 0)
         __syncthreads();
+        RSTAMP(2);                                     // wait for the block
         // (every barrier below is reached by all five waves: the DMA wave's threads have le >= 64)
         const int le = tidv >> 2, q = tidv & 3;
         if (s_tmask) {
@@ -1370,6 +1381,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             if (tidv < ne) apply_vis(s_stk + tidv * FROW + 1);
             __syncthreads();
         }
+        RSTAMP(3);                                     // terminal rows + render
         if (!dmaw) {
             // rows out: per wave (its 16 rows, no barrier) or, after process_vis, per block
             const bool wave_rows = !VIS;
@@ -1388,7 +1400,13 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         // the DMA wave: this step's prefetches have landed before the next step reads them
         if (dmaw) __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
+        RSTAMP(4);                                     // rows out + the block barrier
     }
+#ifdef MGX_RSTAMPS
+    if (tid == 0)
+        for (int k = 0; k < 4; k++) atomicAdd(&p.counters[4 + k], rs_c[k]);
+#endif
+#undef RSTAMP
     // ---- write back: state and ring head (wave 0), every grid, counters; the DMA wave: cur_rng of
     // the envs that popped at the last step
     if (dmaw && lane < ne && K > 0) {

@@ -14,8 +14,8 @@ for cfg in ${CFGS:-2 4 5}; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/s_${cfg}_$lay -o run --output-format csv -- python3 $B > $O/s_${cfg}_$lay.log 2>&1 || { tail -20 $O/s_${cfg}_$lay.log; exit 1; }
     timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $O/f_${cfg}_$lay -o run -- python3 $B > $O/f_${cfg}_$lay.log 2>&1 || { tail -20 $O/f_${cfg}_$lay.log; exit 1; }
     timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $O/w_${cfg}_$lay -o run -- python3 $B > $O/w_${cfg}_$lay.log 2>&1 || { tail -20 $O/w_${cfg}_$lay.log; exit 1; }
-    if [ $lay = fused ]; then K=mgx_rollout_kernel; SPL=32; else K="mgx_step_kernel<int, true>"; SPL=1; fi
+    if [ $lay = fused ]; then K=mgx_rollout_kernel; SPL=64; else K="mgx_step_kernel<int, true>"; SPL=1; fi
     python3 $R/tools/pmc_summary.py $O/f_${cfg}_$lay/run_counter_collection.csv $O/w_${cfg}_$lay/run_counter_collection.csv "$K" ${N[$cfg]} ${S[$cfg]} ${M[$cfg]} $SPL $O/pmc_${cfg}_$lay.json
-    python3 $R/tools/pmc_summary.py $O/f_${cfg}_$lay/run_counter_collection.csv $O/w_${cfg}_$lay/run_counter_collection.csv "mgx_refill" ${N[$cfg]} ${S[$cfg]} ${M[$cfg]} 32 $O/pmc_refill_${cfg}_$lay.json
+    python3 $R/tools/pmc_summary.py $O/f_${cfg}_$lay/run_counter_collection.csv $O/w_${cfg}_$lay/run_counter_collection.csv "mgx_refill" ${N[$cfg]} ${S[$cfg]} ${M[$cfg]} 64 $O/pmc_refill_${cfg}_$lay.json
   done
 done
