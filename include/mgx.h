@@ -141,7 +141,7 @@ mgx_status mgx_destroy(mgx_handle *h);
  * calls follow SB3: seeded (PCG64 only) if mgx_set_seed was called since the
  * last reset, else unseeded; both streams continue from each env's current
  * episode, and mission_done / the stored reward persist.
- * It also pre-generates ring_depth episodes per env (on `stream`; ~6.5 ms at
+ * It also pre-generates ring_depth episodes per env (on `stream`; ~13 ms at
  * 65,536 envs, S = 8).  `livelock_dev` (optional i32 [N]). */
 mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, void *stream);
 
@@ -154,7 +154,7 @@ mgx_status mgx_set_seed(mgx_handle *h, int64_t seed);
 /* One vectorised step.  actions_dev: [N] int32 (action_bytes = 4) or int64 (8).
  * Episode pre-generation runs CONCURRENTLY with the steps on a handle-owned
  * side stream, in epochs of K = refill_every calls: the first call of an epoch
- * joins the previous epoch's refill into `stream`, publishes its episodes and
+ * joins the previous epoch's refill (and the slide that publishes its episodes) and
  * forks the next refill off `stream`.  Whatever the caller enqueues between two
  * epochs (GAE, the policy) overlaps the refill's tail.  The launch sequence
  * depends only on the call count; end a stream capture (hipGraph) with mgx_join

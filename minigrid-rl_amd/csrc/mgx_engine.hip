@@ -439,6 +439,24 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
     }
 }
 
+// Block barrier ordering LDS only.  __syncthreads() is a workgroup fence over every address space: each
+// wave waits for ALL its vector-memory operations (vmcnt(0)) before the barrier -- the DMA wave for the
+// episode prefetches it has just issued, the render waves for their row stores -- and the whole block
+// waits with it.  In the rollout loop nothing crosses a barrier through global memory: the DMA wave's
+// LDS-DMA fills are waited explicitly (s_waitcnt 0) before the end-of-step barrier, the stores are
+// only read by later kernels.  (mgx_step_kernel likewise: its phase-1 loads are waited explicitly.)
+// An LDS-only fence does not do: LDS-DMA fills are LDS writes counted by vmcnt, so a release on LDS
+// still waits for them.  Hence the barrier as inline asm -- lgkmcnt(0) (this wave's LDS reads and
+// writes are done) and s_barrier -- with a memory clobber, so that the compiler moves no memory
+// access across it.
+__device__ __forceinline__ void sync_lds() {
+#ifdef MGX_SYNC_FULL                 // A/B builds: the full workgroup fence
+    __syncthreads();
+#else
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+}
+
 // =============================================================== step kernel
 // Grids in the step kernel's LDS are chunk-major, [GS/16][64 lanes][16 B] (the LDS-DMA
 // layout: one 16-B chunk per lane per global_load_lds); byte b of lane le's grid:
@@ -745,7 +763,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             // (no register load here: its phi copy after the branch would wait on the DMA above)
         }
     }
-    __syncthreads();
+    sync_lds();
 #ifdef MGX_STAMPS
     ts1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -842,7 +860,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     }
     if (my_err) atomicOr(p.err, my_err);
     if (wave1) __builtin_amdgcn_s_waitcnt(0);          // the auto-reset prefetch has landed in LDS
-    __syncthreads();
+    sync_lds();
     // SubprocVecEnv auto-reset: the env takes the popped episode (its header and RNG snapshot
     // were prefetched by wave 1 under the step logic).
     if (popped) {
@@ -922,14 +940,14 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             const int le = tid >> 2, q = tid & 3;
             if (le < ne && s_term[le]) render_cols(s_grid, S, le, q, s_rp[le], s_stk + le * FSTRIDE + FOFF);
         }
-        __syncthreads();
+        sync_lds();
         if (p.vis) {
             if (tid < ne && s_term[tid]) apply_vis(s_stk + tid * FSTRIDE + FOFF);
-            __syncthreads();
+            sync_lds();
         }
         if (COMPACT) {                                // terminal row: byte 0 direction, then the frame
             if (tid < ne && s_term[tid]) s_stk[tid * FROW] = (uint8_t)((s_rp[tid] >> 16) & 3);
-            __syncthreads();
+            sync_lds();
             const int le = tid >> 2, q = tid & 3;
             if (le < ne && s_term[le]) {
                 const uint32_t *fr = reinterpret_cast<const uint32_t *>(s_stk + le * FROW);
@@ -946,7 +964,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
                 for (int k = 37 * q; k < min(37 * q + 37, FRAME); k++) t[k] = fr[k];
             }
         }
-        __syncthreads();
+        sync_lds();
     }
     // ---- phase 2c: one render pass for the whole block (all 256 threads, 4 per env): the
     // newest frame of every env -- the first frame of the new episode where one was popped
@@ -963,10 +981,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // COMPACT without process_vis: each wave copies out the 16 rows it rendered itself (below),
     // no block barrier -- the waves leave the lock-step here
     const bool wave_rows = COMPACT && !p.vis;
-    if (!wave_rows) __syncthreads();
+    if (!wave_rows) sync_lds();
     if (p.vis) {                                       // see_through_walls=False: process_vis
         if (tid < ne) apply_vis(s_stk + tid * FSTRIDE + FOFF);
-        __syncthreads();
+        sync_lds();
     }
 #ifdef MGX_STAMPS
     tsB = __builtin_amdgcn_s_memtime();
@@ -1081,7 +1099,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
                     else if (j == 110) trow[4 * 110] = (uint8_t)(o36 >> 24);
                 }
             }
-            __syncthreads();
+            sync_lds();
             if (kt < limit) reinterpret_cast<uint32_t *>(o.img + e0 * (int64_t)IMG)[kt] = tv;
         }
     } else {
@@ -1155,6 +1173,7 @@ struct ROut {
 };
 constexpr int ROLL_THREADS = BLOCK_THREADS + 64;
 
+
 template <bool VIS>   // see_through_walls == False (Grid.process_vis): its code only in the variant that needs it
 __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p, ROut o, const int32_t *__restrict__ actions,
                                                                       int K) {
@@ -1226,6 +1245,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         p.cur_rng[2 * (e0 + lane)] = r0;
         p.cur_rng[2 * (e0 + lane) + 1] = r1;
     };
+    rpos_t head0 = 0;                                // the DMA wave: this env's ring head at the launch's start
     if (dmaw && lane < ne) {
         __builtin_amdgcn_global_load_lds(actions + e0 + lane, s_act, 4, 0, 0);
         // the end of the env's published episodes: ring_pubn, read ONCE (the slide after a refill running
@@ -1233,6 +1253,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         // with the step wave through s_pub so that the staging and the pops agree
         const rpos_t rhead = p.ring_head[e0 + lane];
         const rpos_t rpub = *reinterpret_cast<volatile const rpos_t *>(p.ring_pubn + e0 + lane);
+        head0 = rhead;
         s_pub[lane] = rpub;
         const int q = (rpos_t)(rpub - rhead);
         if (q > 0) stage(rhead);
@@ -1260,13 +1281,14 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         const int lanev = tidv & (BLOCK_ENVS - 1);
         if (dmaw) {
             // the next step's actions; the ring episode after next of every env that popped last step
+            // (LDS-DMA only: a register load here would make the wave wait for it -- and for every
+            // prefetch in flight -- before the post-logic barrier, the whole block with it)
             if (lanev < ne) {
                 if (t + 1 < K)
                     __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lanev, s_act + (tb ^ 1) * BLOCK_ENVS,
                                                      4, 0, 0);
                 const uint32_t nh = s_nh[tb ^ 1][lanev];
                 if (nh != NO_POP && (rpos_t)(s_pub[lanev] - nh) > 1) stage((rpos_t)(nh + 1));
-                if (nh != NO_POP) rng_out((rpos_t)(nh - 1));
             }
         } else if (wave0) {
             // ---- the step: one lanev per env
@@ -1340,7 +1362,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             if (lanev == 0) s_tmask = tm;
         }
         RSTAMP(1);                                     // step logic (wave 0)
-        __syncthreads();
+        sync_lds();
         RSTAMP(2);                                     // wait for the block
         // (every barrier below is reached by all five waves: the DMA wave's threads have le >= 64)
         const int le = tidv >> 2, q = tidv & 3;
@@ -1348,20 +1370,20 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             // terminal rows (rare, block-uniform): the finished episode's last view, rendered into the
             // env's frame row from its post-step grid and copied out before the row is reused below
             if (le < ne && s_term[le]) render_cols(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW + 1);
-            __syncthreads();
+            sync_lds();
             if (VIS) {
                 if (tidv < ne && s_term[tidv]) apply_vis(s_stk + tidv * FROW + 1);
-                __syncthreads();
+                sync_lds();
             }
             if (tidv < ne && s_term[tidv]) s_stk[tidv * FROW] = (uint8_t)((s_rpt[tidv] >> 16) & 3);
-            __syncthreads();
+            sync_lds();
             if (le < ne && s_term[le]) {
                 const uint32_t *fr = reinterpret_cast<const uint32_t *>(s_stk + le * FROW);
                 uint32_t *tr = reinterpret_cast<uint32_t *>(o.t_rows + (e0 + le) * (int64_t)FROW);
 #pragma unroll 1
                 for (int k = 10 * q; k < min(10 * q + 10, FROW / 4); k++) tr[k] = fr[k];
             }
-            __syncthreads();
+            sync_lds();
         }
         // the frame of every env: the new episode's first where one was popped (rendered straight from
         // its staged grid, which then becomes the env's grid)
@@ -1377,9 +1399,9 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                         *reinterpret_cast<const uint4 *>(g + c * (BLOCK_ENVS * 16) + le * 16);
         }
         if (VIS) {
-            __syncthreads();
+            sync_lds();
             if (tidv < ne) apply_vis(s_stk + tidv * FROW + 1);
-            __syncthreads();
+            sync_lds();
         }
         RSTAMP(3);                                     // terminal rows + render
         if (!dmaw) {
@@ -1399,7 +1421,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         }
         // the DMA wave: this step's prefetches have landed before the next step reads them
         if (dmaw) __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
+        sync_lds();
         RSTAMP(4);                                     // rows out + the block barrier
     }
 #ifdef MGX_RSTAMPS
@@ -1409,10 +1431,11 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
 #undef RSTAMP
     // ---- write back: state and ring head (wave 0), every grid, counters; the DMA wave: cur_rng of
     // the envs that popped at the last step
-    if (dmaw && lane < ne && K > 0) {
-        const uint32_t nh = s_nh[(K - 1) & 1][lane];
-        if (nh != NO_POP) rng_out((rpos_t)(nh - 1));
-    }
+    // cur_rng of every env that popped in this launch: the RNG snapshot of its last pop, once, at the end
+    // (round 3: copied a step after every pop, the DMA wave's register loads made it wait before the
+    // post-logic barrier).  Meanwhile only the MT slider reads cur_rng, and an older cursor is a lower
+    // bound of the live ones.
+    if (dmaw && lane < ne && s_head[lane] != head0) rng_out((rpos_t)(s_head[lane] - 1));
     if (wave0 && lane < ne) {
         reinterpret_cast<uint4 *>(p.state)[e0 + lane] = s_st[lane];
         p.ring_head[e0 + lane] = s_head[lane];
