@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mgx_diag.h"
+
 namespace mgx {
 
 // ---------------------------------------------------------------- cell code
@@ -301,7 +303,7 @@ struct Gen {
     uint32_t tmask;        // bit t: an object of type t is in objs
     // config
     int problem, cfg_mission, num_objects, all_doors_open, n_obstacles;
-#ifdef MGX_GEN_STAMPS
+#if MGX_GEN_STAMPS
     unsigned long long *stamps;   // diagnostic build: per-section wave clocks (counters[8..])
     uint64_t tlast;
 #endif
@@ -309,7 +311,7 @@ struct Gen {
 
 // Diagnostic section clock (MGX_GEN_STAMPS builds only): the first active lane of
 // the wave adds the shader clocks since this lane's previous stamp to counter k.
-#ifdef MGX_GEN_STAMPS
+#if MGX_GEN_STAMPS
 #define GSTAMP(G, k)                                                                     \
     do {                                                                                 \
         const uint64_t _t = __builtin_amdgcn_s_memtime();                                \
@@ -331,12 +333,7 @@ struct Gen {
 #define GCOUNT(G, k) do { } while (0)
 #endif
 
-// Diagnostics only (timing by elimination; episodes are then NOT the reference's): skip generator
-// sections, bit 1 keys + objects, 2 door positions, 4 goal + agent, 8 walls + door draws; inside the
-// keys + objects loop: 16 the MT top-up, 32 the object choice draw.
-#ifndef MGX_GEN_SKIP
-#define MGX_GEN_SKIP 0
-#endif
+// MGX_GEN_SKIP (mgx_diag.h): elimination builds that skip generator sections.
 
 template <int NW>
 __device__ __forceinline__ void put(Gen<NW> &G, int x, int y, uint8_t code) {   // grid.set(x, y, obj)

@@ -1,0 +1,62 @@
+// mgx_diag.h -- every diagnostic and A/B switch of the engine, in one place.
+//
+// The product build (`make -C minigrid-rl_amd`, __graft_entry__.build()) defines none of them and the
+// product library reads no environment variable: its scheduling is fixed at compile time.  Each switch
+// is a build of its own, loaded instead of libmgx.so through MGX_LIB_PATH (mgx/_lib.py), e.g.
+//
+//   make -C minigrid-rl_amd EXTRA="-DMGX_RSTAMPS=1" OUT=mgx/libmgx_rstamps.so
+//   MGX_LIB_PATH=$PWD/minigrid-rl_amd/mgx/libmgx_rstamps.so python tools/diag_rollout_phases.py
+//
+// Clocks are s_memtime cycles summed into the device counters (mgx_debug_counters).
+#pragma once
+
+// ---- clocks ------------------------------------------------------------------------------------
+#ifndef MGX_STAMPS          // mgx_step_kernel phase clocks -> counters[4..7] (1, 2, 3: phase groupings)
+#define MGX_STAMPS 0
+#endif
+#ifndef MGX_RSTAMPS         // mgx_rollout_kernel: wave 0's clocks per phase, summed over the steps -> counters[4..7]
+#define MGX_RSTAMPS 0
+#endif
+#ifndef MGX_REFILL_CLOCK    // refill wave clocks, attempt rounds (busiest lane) and a histogram -> counters[8..29]
+#define MGX_REFILL_CLOCK 0
+#endif
+#ifndef MGX_GEN_STAMPS      // generator section clocks (1: + iteration counts, 2: clocks only).  They inflate the
+#define MGX_GEN_STAMPS 0    // wave's time ~5x (a global atomic per stamp): elimination (MGX_GEN_SKIP) is the measure
+#endif
+
+// ---- elimination builds: the outputs are then NOT the reference's -------------------------------
+#ifndef MGX_GEN_SKIP        // skip generator sections: 1 keys + objects, 2 door positions, 4 goal + agent,
+#define MGX_GEN_SKIP 0      // 8 walls + door draws; inside the keys + objects loop 32 the object choice draw
+#endif
+#ifndef MGX_DIAG_SKIP       // mgx_step_kernel: skip store classes (2 stack roll, 4 missions, 16 grids)
+#define MGX_DIAG_SKIP 0
+#endif
+
+// ---- A/B variants of product choices (the defaults ARE the product) ----------------------------
+#ifndef MGX_NT_STACK        // non-temporal image-stack stores in the SB3 layout
+#define MGX_NT_STACK 0
+#endif
+#ifndef MGX_SYNC_FULL       // mgx_step_kernel: full __syncthreads() instead of the LDS-only barrier
+#define MGX_SYNC_FULL 0
+#endif
+#ifndef MGX_MT_TOPUP        // wave-uniform MT window top-up at this many groups left (0: each lane reloads its
+#define MGX_MT_TOPUP 0      // window when it runs out)
+#endif
+#ifndef MGX_SERIAL_REFILL   // refill on the caller's stream (the refill alone, for timing it)
+#define MGX_SERIAL_REFILL 0
+#endif
+#ifndef MGX_STEP_PRIO       // s_setprio of the per-step kernel's waves (0..3)
+#define MGX_STEP_PRIO 0
+#endif
+#ifndef MGX_REFILL_PRIO     // s_setprio of the refill's waves over co-resident step / rollout waves (0..3)
+#define MGX_REFILL_PRIO 2
+#endif
+#ifndef MGX_REFILL_GENERIC  // 1: problem 'multi' refills with the all-problems kernel, not the multi-only one
+#define MGX_REFILL_GENERIC 0
+#endif
+#ifndef MGX_REFILL_MEAN     // per-wave production cap: 0 the fixed cfg cap, 1 the wave's mean deficit, 2 the
+#define MGX_REFILL_MEAN 2   // wave's mean consumption since its previous refill, rounded up
+#endif
+#ifndef MGX_REFILL_ROUNDS   // grid-wide ceiling of a wave's attempt rounds per epoch: 2 the Bresenham round cap
+#define MGX_REFILL_ROUNDS 1 // of mgx_mt_slide_kernel (round 4), 1 the grid's mean consumption + 1/4 rounded up
+#endif                      // (round 3), 0 none

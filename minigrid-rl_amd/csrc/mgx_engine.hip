@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/mgx.h"
+#include "mgx_diag.h"
 #include "mgx_device.h"
 
 using namespace mgx;
@@ -37,9 +38,6 @@ namespace {
 // the step kernel must stay at <= 112 VGPRs and the refill at <= 176.  LDS: 4 x refill
 // (17.4 KB at the BASELINE configs) + 3 x step (25.8 KB) <= 160 KB.  Check with
 // `make resource-usage` after any change to either kernel.
-#ifndef MGX_DIAG_SKIP
-#define MGX_DIAG_SKIP 0     // diagnostics only: skip store classes (1 pass-1, 2 pass-2, 4 missions, 16 grids)
-#endif
 constexpr int BLOCK_ENVS = 64;
 typedef uint16_t rpos_t;                    // episode ring positions (mod 2^16)
 constexpr int MGX_MAX_RING = 4096;          // ring depth bound (a power of two, far below 2^16)
@@ -73,6 +71,11 @@ struct MtCtl {
     // refill production ceiling (mgx_refill_kernel): the episodes every env popped between the last two
     // refill launches, summed by the slide that follows the last one (running sum, result)
     unsigned long long cons_run, cons_last;
+    // grid-wide ceiling of a refill wave's attempt rounds (MGX_REFILL_ROUNDS 2): round_cap episodes per env
+    // for the next launch, from a fixed-point (1/1024) accumulator of the target production per epoch, so
+    // that the ceiling alternates between floor and ceil of the target instead of always rounding up
+    unsigned long long round_acc;
+    int round_cap, round_pad;
 };
 constexpr int MT_SB_WORDS = 3120;                         // lcm(624, 10): five MT blocks = 312 whole groups
 constexpr int MT_SB_GROUPS = MT_SB_WORDS / MT_FIELDS;
@@ -138,8 +141,6 @@ struct KParams {
     int refill_prio;        // s_setprio of the refill's waves (env MGX_REFILL_PRIO, 0..3)
     int prod_mean;          // refill production cap per wave (env MGX_REFILL_MEAN): 0 fixed `cap`,
                             // 1 the wave's mean deficit (<= cap), 2 its mean consumption, rounded up
-    int cap_max;            // ceiling of that per-wave cap (env MGX_REFILL_CAPMAX): > 0 fixed, 0 none,
-                            // -1 (default) the previous launch's mean consumption per env + 1/4, rounded up
     uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
                             //        generation (mgx_scene regenerates it), else null
 };
@@ -189,7 +190,7 @@ __device__ __forceinline__ unsigned long long wave_uniform64(unsigned long long 
 
 // Image-stack stores (diagnostic switch: -DMGX_NT_STACK = non-temporal)
 __device__ __forceinline__ void stk_store(uint4 *p, uint4 v) {
-#ifdef MGX_NT_STACK
+#if MGX_NT_STACK
     __builtin_nontemporal_store(v.x, &p->x);
     __builtin_nontemporal_store(v.y, &p->y);
     __builtin_nontemporal_store(v.z, &p->z);
@@ -312,7 +313,7 @@ __device__ __forceinline__ void load_gen(Gen<NW> &G, const KParams &p, int64_t e
     G.nobjs = 0;
     G.ax = G.ay = -1;
     G.adir = 0;
-#ifdef MGX_GEN_STAMPS
+#if MGX_GEN_STAMPS
     G.stamps = p.counters;
     G.tlast = __builtin_amdgcn_s_memtime();
 #endif
@@ -452,7 +453,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
 // writes are done) and s_barrier -- with a memory clobber, so that the compiler moves no memory
 // access across it.
 __device__ __forceinline__ void sync_lds() {
-#ifdef MGX_SYNC_FULL                 // A/B builds: the full workgroup fence
+#if MGX_SYNC_FULL                 // A/B builds: the full workgroup fence
     __syncthreads();
 #else
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -643,7 +644,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     if (p.step_prio == 1) __builtin_amdgcn_s_setprio(1);
     else if (p.step_prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (p.step_prio == 3) __builtin_amdgcn_s_setprio(3);
-#ifdef MGX_STAMPS
+#if MGX_STAMPS
     const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
     unsigned long long ts1 = 0, ts2 = 0, tsA = 0, tsB = 0, tsC = 0;
 #endif
@@ -766,7 +767,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         }
     }
     sync_lds();
-#ifdef MGX_STAMPS
+#if MGX_STAMPS
     ts1 = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -905,7 +906,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         }
     }
 
-#ifdef MGX_STAMPS
+#if MGX_STAMPS
     tsA = __builtin_amdgcn_s_memtime();
 #endif
     // ---- phase 2b: mission stacks first (their stores drain during the render), block-
@@ -988,7 +989,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         if (tid < ne) apply_vis(s_stk + tid * FSTRIDE + FOFF);
         sync_lds();
     }
-#ifdef MGX_STAMPS
+#if MGX_STAMPS
     tsB = __builtin_amdgcn_s_memtime();
 #endif
     const int nd = s_nd;
@@ -1002,7 +1003,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             for (int off = q; off < IMG - FRAME; off += 4) t[off] = old[off + FRAME];
         }
     }
-#ifdef MGX_STAMPS
+#if MGX_STAMPS
     ts2 = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -1116,7 +1117,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         }
     }
 
-#ifdef MGX_STAMPS
+#if MGX_STAMPS
     tsC = __builtin_amdgcn_s_memtime();
 #endif
     if (tid == 0) {
@@ -1124,7 +1125,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         atomicAdd(&p.blk[blockIdx.x].x, (unsigned long long)ne);
         if (nd) atomicAdd(&p.blk[blockIdx.x].y, (unsigned long long)nd);
         if (s_ll) atomicAdd(&p.blk[blockIdx.x].z, s_ll);
-#ifdef MGX_STAMPS
+#if MGX_STAMPS
         const unsigned long long ts4 = __builtin_amdgcn_s_memtime();
         atomicAdd(&p.counters[4], ts1 - ts0);   // phase 1: loads
         atomicAdd(&p.counters[5], tsA - ts1);   // phase 2a: step logic
@@ -1240,21 +1241,19 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + c * (BLOCK_ENVS * 16), 16, 0, 0);
         }
     };
-    // cur_rng of an env that popped ring position h (its RNG snapshot; plain loads + stores)
-    auto rng_out = [&](rpos_t h) {
-        const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + (h & (D - 1));
-        const uint4 r0 = p.ring_rng[2 * slot], r1 = p.ring_rng[2 * slot + 1];
-        p.cur_rng[2 * (e0 + lane)] = r0;
-        p.cur_rng[2 * (e0 + lane) + 1] = r1;
-    };
     rpos_t head0 = 0;                                // the DMA wave: this env's ring head at the launch's start
     if (dmaw && lane < ne) {
         __builtin_amdgcn_global_load_lds(actions + e0 + lane, s_act, 4, 0, 0);
         // the end of the env's published episodes: ring_pubn, read ONCE (the slide after a refill running
         // beside this launch may raise it meanwhile; every value it takes is a completed refill's), shared
         // with the step wave through s_pub so that the staging and the pops agree
+        // Visibility of the slots below the value read: every value ring_pubn takes is the tail of a refill
+        // that has COMPLETED (the slide that writes it follows the refill on the refill stream), and a kernel's
+        // stores are released at its end.  The agent-scope load bypasses this CU's L1; the slot lines
+        // themselves are read by this env's workgroup alone (env-contiguous rings), after this load and
+        // after the launch's own L1 invalidate, so no line of them can be stale here.
         const rpos_t rhead = p.ring_head[e0 + lane];
-        const rpos_t rpub = *reinterpret_cast<volatile const rpos_t *>(p.ring_pubn + e0 + lane);
+        const rpos_t rpub = __hip_atomic_load(p.ring_pubn + e0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         head0 = rhead;
         s_pub[lane] = rpub;
         const int q = (rpos_t)(rpub - rhead);
@@ -1264,7 +1263,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 
-#ifdef MGX_RSTAMPS
+#if MGX_RSTAMPS
     // diagnostics (-DMGX_RSTAMPS): wave 0's clocks per phase, summed over the steps -> counters[4..7]
     unsigned long long rs_c[4] = {0, 0, 0, 0}, rs_t = 0;
 #define RSTAMP(k) do { if (tid == 0) { const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
@@ -1426,7 +1425,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         __syncthreads();
         RSTAMP(4);                                     // rows out + the block barrier
     }
-#ifdef MGX_RSTAMPS
+#if MGX_RSTAMPS
     if (tid == 0)
         for (int k = 0; k < 4; k++) atomicAdd(&p.counters[4 + k], rs_c[k]);
 #endif
@@ -1437,7 +1436,22 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     // (round 3: copied a step after every pop, the DMA wave's register loads made it wait before the
     // post-logic barrier).  Meanwhile only the MT slider reads cur_rng, and an older cursor is a lower
     // bound of the live ones.
-    if (dmaw && lane < ne && s_head[lane] != head0) rng_out((rpos_t)(s_head[lane] - 1));
+    // The snapshot is LOADED before the new head is published (a barrier between them): once ring_head
+    // moves, a refill running beside this launch may reuse that slot (the head store raced the
+    // load).  Stored to cur_rng after the barrier.
+    uint4 rng0 = make_uint4(0, 0, 0, 0), rng1 = rng0;
+    const bool rng_w = dmaw && lane < ne && s_head[lane] != head0;
+    if (rng_w) {
+        const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + ((rpos_t)(s_head[lane] - 1) & (D - 1));
+        rng0 = p.ring_rng[2 * slot];
+        rng1 = p.ring_rng[2 * slot + 1];
+    }
+    if (dmaw) __builtin_amdgcn_s_waitcnt(0);         // the loads have returned ...
+    __syncthreads();                                 // ... before wave 0 stores the heads below
+    if (rng_w) {
+        p.cur_rng[2 * (e0 + lane)] = rng0;
+        p.cur_rng[2 * (e0 + lane) + 1] = rng1;
+    }
     if (wave0 && lane < ne) {
         reinterpret_cast<uint4 *>(p.state)[e0 + lane] = s_st[lane];
         p.ring_head[e0 + lane] = s_head[lane];
@@ -1544,7 +1558,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     if (p.refill_prio == 1) __builtin_amdgcn_s_setprio(1);
     else if (p.refill_prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (p.refill_prio == 3) __builtin_amdgcn_s_setprio(3);
-#ifdef MGX_REFILL_CLOCK
+#if MGX_REFILL_CLOCK
     const unsigned long long rc0 = __builtin_amdgcn_s_memtime();   // diagnostics: wave clocks per launch
     int rc_iters = 0;
 #endif
@@ -1582,8 +1596,16 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         }
         cnt = max(cnt, 1);
         cap = by_cons ? (sum + cnt - 1) / cnt : min(cap, (2 * sum + cnt) / (2 * cnt));
-        if (p.cap_max > 0) cap = min(cap, p.cap_max);
-        if (p.cap_max < 0 && by_cons) {
+        if (MGX_REFILL_ROUNDS == 2 && by_cons) {
+            // The launch lasts as long as its slowest wave, and a wave runs as many attempt rounds as its
+            // cap: one ceiling common to all waves (mgx_mt_slide_kernel: the grid's mean consumption per env
+            // plus a margin, in whole rounds whose average is that target) keeps the waves whose lanes
+            // popped more than the rest from setting the launch.  Their lanes keep the difference as a
+            // deficit, which the ring depth absorbs and later epochs pay back.
+            const int rc = p.mtc->round_cap;                       // wave-uniform (scalar load)
+            if (rc > 0) cap = min(cap, rc);
+        }
+        if (MGX_REFILL_ROUNDS == 1 && by_cons) {
             // The launch lasts as long as its slowest wave, and a wave runs as many attempt rounds as
             // its cap: a ceiling common to all waves keeps the few waves whose lanes popped more than
             // the rest (one in ten would round up to 6 at config 2) from setting the launch.  Their
@@ -1614,7 +1636,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
             // episode of this epoch's production (unless the invariant needs it), not the wave an
             // extra round -- the retry then continues in the next epoch, its count carried in aux.
             while (nfree > 0) {
-#ifdef MGX_REFILL_CLOCK
+#if MGX_REFILL_CLOCK
                 rc_iters++;
 #endif
                 ResetOut R;
@@ -1659,11 +1681,11 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         unsigned long long o = __shfl_down(maxcur, off);
         maxcur = o > maxcur ? o : maxcur;
         err |= __shfl_down(err, off);
-#ifdef MGX_REFILL_CLOCK
+#if MGX_REFILL_CLOCK
         rc_iters = max(rc_iters, __shfl_down(rc_iters, off));
 #endif
     }
-#ifdef MGX_REFILL_CLOCK
+#if MGX_REFILL_CLOCK
     if (tid == 0) {
         atomicAdd(&p.counters[26], __builtin_amdgcn_s_memtime() - rc0);   // wave clocks
         atomicAdd(&p.counters[27], (unsigned long long)rc_iters);          // attempt rounds (busiest lane)
@@ -1832,7 +1854,25 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     if (s_nsb < 0) return;
     if (tid == 0) {
         __threadfence();
-        c->cons_last = atomicExch(&c->cons_run, 0ull);   // the last refill's consumption, all envs
+        const unsigned long long cons = atomicExch(&c->cons_run, 0ull);   // the last refill's consumption, all envs
+        c->cons_last = cons;
+        if (cons && p.D > 0 && p.n > 0) {
+            // Round cap of the next refill (MGX_REFILL_ROUNDS 2): target production per env per epoch =
+            // mean consumption + a margin m, so the lanes' levels drift up by m per epoch and only rarely
+            // fall to the invariant's 2K (need-driven rounds).  A lane's deficit is a random walk with
+            // per-epoch variance ~ mean (resets are ~Bernoulli per step); with drift m its stationary tail
+            // is ~exp(-2 m x / mean), so m = 9 mean / (D - 2K) puts the 2K floor >= 18 e-folds away.  At
+            // E = 64 (D = 256) that is 10.0 rounds (round 3's ceil(mean + 1/4) = 10 too); at the 20-step
+            // epochs of the driver's line 3.04 (round 3: 4), i.e. 3 rounds in 24 epochs of 25.
+            const double mean = (double)cons / (double)p.n;
+            const double slack = (double)max(p.D - 2 * p.K, 1);
+            const double tgt = mean * (1.0 + 9.0 / slack);
+            const unsigned long long acc0 = c->round_acc;
+            const unsigned long long acc1 = acc0 + (unsigned long long)(tgt * 1024.0 + 0.5);
+            const int r = (int)((acc1 >> 10) - (acc0 >> 10));
+            c->round_acc = acc1;
+            c->round_cap = r > 1 ? r : 1;
+        }
         const unsigned long long m = atomicExch(&c->span_min, ~0ull);   // every workgroup's extremes; reset
         const unsigned long long x = atomicExch(&c->span_max, 0ull);
         c->done = 0;
@@ -2388,23 +2428,15 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->calls = 0;
     h->in_flight = false;
     h->pub_stale = true;
-    {
-        const char *sv = std::getenv("MGX_SERIAL_REFILL");
-        h->serial_refill = sv && sv[0] == '1';
-        const char *st = std::getenv("MGX_STEP_PRIO");
-        h->kp.step_prio = st ? std::atoi(st) : 0;
-        const char *rp = std::getenv("MGX_REFILL_PRIO");
-        // refill waves at issue priority 2 over co-resident step / rollout waves: the refill sets the
-        // pipeline beside the fused rollout (+3-7 % at config 2, +4 % at config 4; per-step layouts
-        // and config 5 within +-0.5 %, tools/gpu_prio3.sh / gpu_prio4.sh)
-        h->kp.refill_prio = rp ? std::atoi(rp) : 2;
-        const char *pm = std::getenv("MGX_REFILL_MEAN");
-        h->kp.prod_mean = pm ? std::atoi(pm) : 2;
-        const char *cm = std::getenv("MGX_REFILL_CAPMAX");
-        h->kp.cap_max = cm ? std::atoi(cm) : -1;
-        const char *rg = std::getenv("MGX_REFILL_GENERIC");
-        h->refill_multi = !(rg && rg[0] == '1');
-    }
+    // scheduling choices: compile-time (mgx_diag.h; A/B builds), never read from the environment
+    h->serial_refill = MGX_SERIAL_REFILL != 0;
+    h->kp.step_prio = MGX_STEP_PRIO;
+    // refill waves at issue priority 2 over co-resident step / rollout waves: the refill sets the
+    // pipeline beside the fused rollout (+3-7 % at config 2, +4 % at config 4; per-step layouts
+    // and config 5 within +-0.5 %, round 3)
+    h->kp.refill_prio = MGX_REFILL_PRIO;
+    h->kp.prod_mean = MGX_REFILL_MEAN;
+    h->refill_multi = MGX_REFILL_GENERIC == 0;
     // MT ring: a power of two of 10-word groups holding at least mt_table_words words (>= 512 groups)
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 26;
     int64_t ring_groups = 512;

@@ -206,21 +206,20 @@ class MgxEngine:
             pass
 
 
-_SCRATCH = {}
-
-
 def _stats_scratch(stats):
-    """The adv-stat shard scratch of the calling stream (include/mgx.h, MGX_GAE_SCRATCH_WORDS): GAE calls
-    on different streams (e.g. two collectors) never share partial sums; calls on one stream are ordered."""
+    """The adv-stat shard scratch (include/mgx.h, MGX_GAE_SCRATCH_WORDS) of this `stats` tensor on the
+    calling stream: GAE calls on different streams (e.g. two collectors) never share partial sums; calls on
+    one stream are ordered.  The scratches live on the stats tensor itself, so they are freed with it (a
+    module-level cache keyed by stream handle kept one per stream handle for the life of the process)."""
     if stats is None:
         return None
     assert stats.dtype == torch.float64 and stats.numel() >= 3 and stats.is_contiguous()
-    stream = torch.cuda.current_stream(stats.device)
-    key = (stats.device.index, stream.cuda_stream)
-    buf = _SCRATCH.get(key)
+    per = stats.__dict__.setdefault("_mgx_scratch", {})
+    key = torch.cuda.current_stream(stats.device).cuda_stream
+    buf = per.get(key)
     if buf is None:
         buf = torch.zeros(_lib.GAE_SCRATCH_WORDS, dtype=torch.float64, device=stats.device)
-        _SCRATCH[key] = buf
+        per[key] = buf
     return buf
 
 

@@ -59,15 +59,17 @@ class Dict:
         return "Dict(%s)" % ", ".join("%s: %r" % kv for kv in self.spaces.items())
 
 
-def make_spaces(n_stack, mission_dtype=np.int64, raw=False):
+def make_spaces(n_stack, mission_dtype=np.int64, raw=False, dir_one_hot=True):
     """(observation_space, action_space) of the stacked, transposed env -- or, raw=True, of one
-    wrapped env as make_vec_env hands it out (environment.py:84-89,142): image HWC (7,7,3)."""
+    wrapped env as make_vec_env hands it out (environment.py:84-89,142): image HWC (7,7,3).
+    dir_one_hot (raw only): make_env applies Discrete2BoxWrapper only when n_frames_stack > 1 and not
+    recurrent (environment.py:28-29); otherwise the direction is MiniGridEnv's own Discrete(4)."""
     mk_box = (lambda lo, hi, shape, dt: _gs.Box(lo, hi, shape, dt)) if _gs else Box
     mk_dict = _gs.Dict if _gs else Dict
     mk_disc = _gs.Discrete if _gs else Discrete
     if raw:
         obs = mk_dict({
-            "direction": mk_box(0, 1, (4,), np.uint8),                 # Discrete2BoxWrapper
+            "direction": mk_box(0, 1, (4,), np.uint8) if dir_one_hot else mk_disc(4),   # Discrete2BoxWrapper | raw
             "image": mk_box(0, 255, (7, 7, 3), np.uint8),              # MiniGridEnv image, [vx][vy][c]
             "mission": mk_box(0, 32, (32,), mission_dtype),            # TokenizeVocabWrapper
         })

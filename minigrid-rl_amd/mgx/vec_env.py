@@ -21,6 +21,15 @@ Two modes:
     (which, not seeing a VecTransposeImage in the chain, would transpose the (3n,7,7) image
     space again: use raw mode with SB3's algorithms).
 
+Raw mode follows make_env's wrapper rule (environment.py:28-29): the direction is the one-hot Box(4,)
+of Discrete2BoxWrapper only when n_frames_stack > 1 and not recurrent; otherwise it is MiniGridEnv's
+Discrete(4) (an int64 per env on the host).
+
+Trajectories are SubprocVecEnv's (ppo.py:121, single_run): each env its own CPython `random`
+(MT19937(seed), custom_env.py:82).  The reference's MULTIRUN branch (`DummyVecEnv`) runs every env in
+one process, whose envs then draw from ONE process-global MT stream interleaved by env index; the
+engine does not reproduce that interleaving (`vec_env_cls="dummy"` with n_envs > 1 warns).
+
 When stable_baselines3 is importable the class subclasses its `VecEnv` (so `_wrap_env` does
 not re-wrap it in a DummyVecEnv); otherwise it duck-types the same contract
 (stable_baselines3.common.vec_env.base_vec_env):
@@ -40,6 +49,7 @@ device (MgxEngine).  This class is for callers that want the reference's host
 API unchanged, at the cost of a device->host copy of the observation per step.
 """
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -65,16 +75,32 @@ class MgxVecEnv(_VecEnvBase):
 
     def __init__(self, n_envs, seed=42, n_frames_stack=4, problem="multi", mission=5, size=8, num_objects=4,
                  all_doors_open=False, see_through_walls=True, obstacles=False, device="cuda",
-                 env_index_offset=0, raw=False, **engine_kw):
+                 env_index_offset=0, raw=False, recurrent=False, vec_env_cls="subproc", **engine_kw):
         self.num_envs = int(n_envs)
         self.raw = bool(raw)
         self.n_stack = 1 if self.raw else int(n_frames_stack)
+        if self.raw:
+            # make_env wraps the direction in Discrete2BoxWrapper only when n_frames_stack > 1 and not
+            # recurrent (environment.py:28-29); otherwise the env hands out MiniGridEnv's Discrete(4)
+            self.dir_one_hot = int(n_frames_stack) > 1 and not recurrent
+        else:
+            if recurrent:
+                raise ValueError("fused mode is VecTransposeImage + VecFrameStack, which the reference applies only "
+                                 "when not recurrent (ppo.py:124): use raw=True")
+            self.dir_one_hot = True
+        if vec_env_cls not in ("subproc", "dummy"):
+            raise ValueError("vec_env_cls must be 'subproc' or 'dummy'")
+        if vec_env_cls == "dummy" and self.num_envs > 1:
+            warnings.warn("MgxVecEnv reproduces SubprocVecEnv trajectories (one CPython random per env, "
+                          "custom_env.py:82); the reference's DummyVecEnv branch (ppo.py:121, multirun) shares one "
+                          "process-global MT19937 stream across its envs, so its trajectories differ for n_envs > 1",
+                          RuntimeWarning, stacklevel=2)
         self.engine = MgxEngine(problem=problem, mission=mission, size=size, num_objects=num_objects,
                                 n_envs=n_envs, seed=seed, env_index_offset=env_index_offset, n_stack=self.n_stack,
                                 all_doors_open=all_doors_open, see_through_walls=see_through_walls,
                                 obstacles=obstacles, terminal_mode="all", reward64=True, device=device,
                                 **engine_kw)
-        obs_space, act_space = make_spaces(self.n_stack, raw=self.raw)
+        obs_space, act_space = make_spaces(self.n_stack, raw=self.raw, dir_one_hot=self.dir_one_hot)
         self.render_mode = None
         self._attrs = dict(problem=problem, mission=mission, size=size, num_objects=num_objects,
                            max_steps=size * size, all_doors_open=all_doors_open,
@@ -90,7 +116,7 @@ class MgxVecEnv(_VecEnvBase):
         dev = self.engine.device
         self._act_dev = torch.zeros(self.num_envs, dtype=torch.int64, device=dev)
         pin = torch.cuda.is_available()
-        self._host = {k: torch.empty(self._host_shape(k, v), dtype=v.dtype, pin_memory=pin)
+        self._host = {k: torch.empty(self._host_shape(k, v), dtype=self._layout(k, v[:1]).dtype, pin_memory=pin)
                       for k, v in self.engine.obs.items()}
         self._host_scalars = torch.empty((4, self.num_envs), dtype=torch.float64, pin_memory=pin)
         self._ep_start = np.full(self.num_envs, time.time())
@@ -193,12 +219,17 @@ class MgxVecEnv(_VecEnvBase):
     def _host_shape(self, key, v):
         if self.raw and key == "image":          # (N, 3, 7, 7) [c][vx][vy] -> the env's (N, 7, 7, 3)
             return (v.shape[0], 7, 7, 3)
+        if key == "direction" and not self.dir_one_hot:
+            return (v.shape[0],)
         return tuple(v.shape)
 
     def _layout(self, key, v):
-        """Engine tensor -> the layout this VecEnv hands out (raw mode: the env's HWC image)."""
+        """Engine tensor -> the layout this VecEnv hands out (raw mode: the env's HWC image; the Discrete(4)
+        direction where make_env adds no Discrete2BoxWrapper)."""
         if self.raw and key == "image":
             return v.permute(0, 2, 3, 1)
+        if key == "direction" and not self.dir_one_hot:
+            return v.argmax(1)                   # one-hot (4,) of the single frame -> int64 direction
         return v
 
     def _obs_to_host(self, obs):

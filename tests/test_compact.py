@@ -153,3 +153,72 @@ def test_graph_replays_equal_eager_steps():
     for k in de:
         a, b = np.asarray(de[k]), np.asarray(dg[k])
         assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), k      # None is stored as NaN
+
+
+GATHER_FIXTURES = [("multi_all_s8", 4), ("multi_gtg_s8", 4), ("multi_pkp_s11", 3), ("multi_tgl_s16", 4),
+                   ("novis_multi_all_s8", 2), ("manual_multi_all_s8", 4)]
+
+
+@pytest.mark.parametrize("name,n_stack", GATHER_FIXTURES, ids=[f[0] + "_k%d" % f[1] for f in GATHER_FIXTURES])
+def test_gather_matches_framestack_oracle_on_fixtures(name, n_stack):
+    """mgx_gather pinned directly to the reference fixtures through the restated SB3 layer
+    (O.FrameStackOracle = VecTransposeImage + VecFrameStack(n_stack, 'first') over the fixture's own
+    per-step observations): the engine steps the fixture's actions in the compact layout; after every
+    step the gathered stack of every env (u8 and f32 = u8 * (1/255), SB3 preprocess_obs) and, where the
+    env finished, the gathered terminal stack (terminal row + older rows) equal the oracle's stack and
+    terminal_observation stack; at the end one random-order minibatch gather over every (t, env) of the
+    rollout equals the stacks recorded along the way."""
+    _need_gpu()
+    import os
+    import oracle as O
+    import trajcheck as TC
+    from mgx import MgxEngine
+    from mgx.compact import CompactBuffer
+    d = dict(np.load(os.path.join(os.path.dirname(TC.__file__), "golden", "traj", name + ".npz")))
+    cfg, T = TC.fixture_cfg(d)
+    T = min(T, 256)
+    kw = dict(cfg)
+    n = kw.pop("n_envs")
+    eng = MgxEngine(n_envs=n, n_stack=n_stack, terminal_mode="all", mission_dtype=torch.uint8, **kw)
+    buf = CompactBuffer(eng, T)
+    fs = O.FrameStackOracle(n, n_stack)
+
+    def raw(img, dr, ms):
+        return dict(image=O.vec_transpose_image(img), direction=O.one_hot_dir(dr), mission=ms.astype(np.int64))
+
+    def check(g, want, f32, tag):
+        if f32:
+            assert np.array_equal(g["image"].cpu().numpy(), want["image"].astype(np.float32) * np.float32(1.0 / 255.0)), tag
+            assert np.array_equal(g["direction"].cpu().numpy(), want["direction"].astype(np.float32)), tag
+        else:
+            assert np.array_equal(g["image"].cpu().numpy(), want["image"]), tag
+            assert np.array_equal(g["direction"].cpu().numpy(), want["direction"]), tag
+        assert np.array_equal(g["mission"].cpu().numpy().astype(np.int64), want["mission"]), tag
+
+    eng.reset()
+    buf.observe(0)
+    stacks = [fs.reset(raw(d["reset0_image"], d["reset0_dir"], d["reset0_mission"]))]
+    check(buf.gather_step(0, f32=False), stacks[0], False, "reset")
+    n_term = 0
+    for t in range(T):
+        buf.step(t, torch.as_tensor(d["actions"][t].astype(np.int32), device=eng.device))
+        done = (d["terminated"][t] | d["truncated"][t]).astype(bool)
+        cur = raw(np.where(done[:, None, None, None], d["r_image"][t], d["image"][t]),
+                  np.where(done, d["r_dir"][t], d["dir"][t]), np.where(done[:, None], d["r_mission"][t], d["mission"][t]))
+        st, term = fs.step(cur, done, raw(d["image"][t], d["dir"][t], d["mission"][t]))
+        stacks.append(st)
+        check(buf.gather_step(t + 1, f32=bool(t % 2)), st, bool(t % 2), ("obs", t))
+        if done.any():
+            envs = np.nonzero(done)[0]
+            n_term += envs.size
+            g = buf.gather_step(t, terminal=True, f32=bool(t % 3 == 0), envs=torch.as_tensor(envs, device=eng.device))
+            check(g, {k: v[envs] for k, v in term.items()}, bool(t % 3 == 0), ("terminal", t))
+    assert n_term > 0
+    eng.poll_error()
+    gen = torch.Generator(device="cpu")
+    gen.manual_seed(5)
+    perm = torch.randperm((T + 1) * n, generator=gen)
+    tt, ee = (perm // n).numpy(), (perm % n).numpy()
+    g = buf.gather(torch.as_tensor((buf.H + tt) * n + ee, device=eng.device), f32=False)
+    want = {k: np.stack([stacks[a][k][b] for a, b in zip(tt, ee)]) for k in ("image", "direction", "mission")}
+    check(g, want, False, "minibatch")

@@ -383,16 +383,17 @@ def test_full_size_matches_oracle(problem, mission, size, n, T, layout):
     eng.poll_error()
 
 
+@pytest.mark.parametrize("layout", ["fused", "compact"])
 @pytest.mark.parametrize("n", [8192, 65536])
-def test_bench_shape_graph_matches_oracle(n):
-    """The exact shape bench.py times (its default and the driver's 20-step line): GTG 8x8,
-    compact layout, terminal_mode 'truncated', refill epoch E = 20 = horizon H, one hipGraph per
-    chunk holding the carry-over, 20 mgx_step_compact launches (the first forks the epoch's
-    refill), mgx_gae_dones with the adv-stat triple and mgx_join -- replayed 4 times with new
-    actions in its static buffer.  Every replay: each step's observation rows, mission ids, dones,
-    terminated / truncated flags and f32 rewards vs the C oracle, the terminal row of every env
-    that was truncated, GAE advantages / returns bit-exact vs numpy and the (sum A, sum A^2, n)
-    triple; at the end every env's state."""
+def test_bench_shape_graph_matches_oracle(n, layout):
+    """The exact shape bench.py times -- the driver's `--steps 20` line: GTG 8x8, terminal_mode
+    'truncated', refill epoch E = 20 = horizon H, one hipGraph per chunk holding the carry-over, the
+    steps, mgx_gae_dones with the adv-stat triple and mgx_join -- replayed 4 times with new actions in
+    its static buffer.  `fused` (the headline): ONE mgx_rollout_compact launch of the 20 steps (it
+    forks the epoch's refill); `compact`: 20 mgx_step_compact launches (the per-step line).  Every
+    replay: each step's observation rows, mission ids, dones, terminated / truncated flags and f32
+    rewards vs the C oracle, the terminal row of every env that was truncated, GAE advantages /
+    returns bit-exact vs numpy and the (sum A, sum A^2, n) triple; at the end every env's state."""
     _need_gpu()
     import oracle as O
     from mgx import MgxEngine, gae_dones
@@ -412,11 +413,17 @@ def test_bench_shape_graph_matches_oracle(n):
     ov.reset()
     eng.reset()
     buf.observe(0)
-    for t in range(W):
+    fused = layout == "fused"
+    for t in range(0, W, E if fused else 1):
         if t and t % E == 0:
             buf.carry_over()
-        buf.step(t % E, torch.as_tensor(acts[t], device=dev))
-        ov.step(acts[t])
+        if fused:
+            buf.rollout(0, torch.as_tensor(acts[t:t + E], device=dev))
+            for j in range(E):
+                ov.step(acts[t + j])
+        else:
+            buf.step(t % E, torch.as_tensor(acts[t], device=dev))
+            ov.step(acts[t])
     eng.join()
     torch.cuda.synchronize()
     vals = torch.as_tensor(rng.standard_normal((E, n)).astype(np.float32), device=dev)
@@ -431,8 +438,11 @@ def test_bench_shape_graph_matches_oracle(n):
         gr.capture_begin()
         st.zero_()
         buf.carry_over()
-        for j in range(E):
-            buf.step(j, static[j])
+        if fused:
+            buf.rollout(0, static)
+        else:
+            for j in range(E):
+                buf.step(j, static[j])
         gae_dones(buf.rewards, vals, buf.dones, last_v, gamma, lam, stats=st, out=(adv, ret))
         eng.join()
         gr.capture_end()

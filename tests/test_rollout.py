@@ -88,10 +88,11 @@ def test_rollout_equals_per_step(case, chunks):
     assert sb["queued"] >= E * n, sb
 
 
-def test_rollout_ring_positions_wrap():
-    """Ring positions are u8 counters (mod 256): over 640 steps with 'done' on 3 of 4 actions every
-    env pops > 256 episodes, so every head passes 255 -> 0 (and takes the value 255, which the fused
-    kernel's 'no pop' marker must not alias).  Fused chunks equal per-step calls bit for bit."""
+def test_rollout_bursts_of_pops():
+    """Over 640 steps with 'done' on 3 of 4 actions every env pops > 300 episodes (pops on most
+    consecutive steps, the staged ring episodes cycling through both LDS buffers).  Fused chunks equal
+    per-step calls bit for bit.  (Ring positions are u16 since round 3: test_ring_positions_wrap_u16
+    runs them past 65,535 -> 0.)"""
     _need_gpu()
     from mgx.compact import CompactBuffer
     n, E, T = 512, 32, 64
@@ -122,20 +123,67 @@ def test_rollout_ring_positions_wrap():
     assert sa["resets"] == sb["resets"] > 300 * n, (sa, sb)
 
 
-@pytest.mark.parametrize("problem,mission,size,n,T", [("multi", 5, 8, 65536, 64), ("multi", 1, 16, 131072, 32)],
-                         ids=["cfg2_65536", "cfg5_131072"])
-def test_rollout_full_size_matches_oracle(problem, mission, size, n, T):
+def test_ring_positions_wrap_u16():
+    """Ring positions (head, tail, pub, pubn, seen) are u16 counters mod 2^16 (rpos_t): with 'done' on
+    97 % of the actions, 64 envs pop > 65,536 episodes each over 69,120 steps, so every position passes
+    65,535 -> 0 -- the (rpos_t)(pub - head) levels, the refill's `tail - head` and `head - seen`, and the
+    `head & (D - 1)` slots across the wrap.  Fused chunks (one launch per 64-step epoch) equal per-step
+    calls bit for bit at every chunk; at the end both engines' states equal the C oracle's."""
+    _need_gpu()
+    import oracle as O
+    from mgx.compact import CompactBuffer
+    n, E = 64, 64
+    nchunk = 1080
+    ref, fus = _engines(dict(problem="multi", mission=5, size=8), n, refill_every=E)
+    ov = O.OracleVec("multi", 5, 8, 4, n, 42)
+    br, bf = CompactBuffer(ref, E), CompactBuffer(fus, E)
+    ref.reset(); fus.reset(); ov.reset()
+    br.observe(0); bf.observe(0)
+    rng = np.random.default_rng(65536)
+    acts = np.where(rng.random((nchunk * E, n)) < 0.97, 6, rng.integers(0, 7, (nchunk * E, n))).astype(np.int32)
+    ad = torch.as_tensor(acts, device=ref.device)
+    for c in range(nchunk):
+        if c:
+            br.carry_over(); bf.carry_over()
+        bf.rollout(0, ad[c * E:(c + 1) * E])
+        for j in range(E):
+            br.step(j, ad[c * E + j])
+        if c % 8 == 7 or c == nchunk - 1:
+            for name in ("rows", "mids", "starts", "rewards", "terminated", "truncated"):
+                assert torch.equal(getattr(br, name), getattr(bf, name)), (c, name)
+            assert torch.equal(br.terminal_rows, bf.terminal_rows), c
+    for t in range(nchunk * E):
+        ov.step(acts[t])
+    ref.poll_error()
+    fus.poll_error()
+    sa, sb = ref.stats(), fus.stats()
+    assert sa["resets"] == sb["resets"] > 65600 * n, (sa, sb)
+    want = ov.dump()
+    for eng in (ref, fus):
+        got = eng.dump_state()
+        for k in ("grid", "agent", "carrying", "step_count", "mission_done", "mtwords", "pcg", "target"):
+            assert np.array_equal(got[k], want[k]), k
+        assert np.array_equal(got["stored_reward"], want["stored_reward"], equal_nan=True)
+
+
+@pytest.mark.parametrize("problem,mission,size,n,T,offset", [("multi", 5, 8, 65536, 64, 0),
+                                                               ("multi", None, 8, 32768, 64, 32768),
+                                                               ("multi", 1, 16, 131072, 32, 0)],
+                         ids=["cfg2_65536", "cfg4_32768_rank1", "cfg5_131072"])
+def test_rollout_full_size_matches_oracle(problem, mission, size, n, T, offset):
     """BASELINE per-GPU sizes: the fused rollout of T steps (whole refill epochs) against the C
-    oracle -- every env's row, done flag and f32 reward at every step, then every env's state."""
+    oracle -- every env's row, done flag and f32 reward at every step, then every env's state.
+    cfg4_32768_rank1 is rank 1's shard of config 4 (ALL mixed 8x8, env_index_offset = 32,768: envs
+    seeded 42 + 32,768 + i), what ranks 1-7 of the 8-GPU bench run."""
     _need_gpu()
     import oracle as O
     from mgx import MgxEngine
     from mgx._lib import mission_tokens
     from mgx.compact import CompactBuffer
     E = 32
-    ov = O.OracleVec(problem, mission, size, 4, n, 42)
+    ov = O.OracleVec(problem, mission, size, 4, n, 42, index_offset=offset)
     eng = MgxEngine(problem=problem, mission=mission, size=size, n_envs=n, terminal_mode="truncated",
-                    mission_dtype=torch.uint8, refill_every=E)
+                    mission_dtype=torch.uint8, refill_every=E, env_index_offset=offset)
     buf = CompactBuffer(eng, T)
     tok = mission_tokens()
     ov.reset()
@@ -243,3 +291,63 @@ def test_rollout_rejects_chunks_across_epochs():
     buf.rollout(10, a[10:16].contiguous())
     buf.rollout(16, a[16:32].contiguous())
     eng.poll_error()
+
+
+@pytest.mark.parametrize("layout", ["fused", "compact"])
+@pytest.mark.parametrize("problem,mission,size,n", [("multi", 5, 8, 4096), ("multi", None, 8, 2048), ("multi", 1, 16, 1024)],
+                         ids=["cfg2", "cfg4", "cfg5"])
+def test_shards_equal_slices_of_one_engine(problem, mission, size, n, layout):
+    """Multi-GPU sharding: rank r owns global envs [r*n, (r+1)*n) through env_index_offset.
+    Two shard engines (offsets 0 and n) against ONE engine of 2n envs, same actions: every output row,
+    mission id, reward, done / terminated / truncated flag, terminal row and counter, and every env's state
+    at the end, is the matching slice of the single engine's, bit for bit -- in the fused rollout (the
+    bench's headline launch) and per step (the PPO path)."""
+    _need_gpu()
+    from mgx import MgxEngine
+    from mgx.compact import CompactBuffer
+    E, T, rolls = 32, 64, 3
+    kw = dict(problem=problem, mission=mission, size=size, terminal_mode="all", mission_dtype=torch.uint8,
+              refill_every=E)
+    whole = MgxEngine(n_envs=2 * n, **kw)
+    shards = [MgxEngine(n_envs=n, env_index_offset=r * n, **kw) for r in range(2)]
+    bw = CompactBuffer(whole, T)
+    bs = [CompactBuffer(s, T) for s in shards]
+    for e, b in [(whole, bw)] + list(zip(shards, bs)):
+        e.reset()
+        b.observe(0)
+    g = torch.Generator(device=whole.device)
+    g.manual_seed(4242)
+    for roll in range(rolls):
+        if roll:
+            for b in [bw] + bs:
+                b.carry_over()
+        acts = torch.randint(0, 7, (T, 2 * n), device=whole.device, generator=g, dtype=torch.int32)
+        for t in range(0, T, E):
+            chunk = acts[t:t + E]
+            if layout == "fused":
+                bw.rollout(t, chunk.contiguous())
+                for r in range(2):
+                    bs[r].rollout(t, chunk[:, r * n:(r + 1) * n].contiguous())
+            else:
+                for j in range(E):
+                    bw.step(t + j, chunk[j])
+                    for r in range(2):
+                        bs[r].step(t + j, chunk[j, r * n:(r + 1) * n].contiguous())
+        for name in ("rows", "mids", "starts", "rewards", "terminated", "truncated"):
+            w = getattr(bw, name)
+            for r in range(2):
+                assert torch.equal(getattr(bs[r], name), w[:, r * n:(r + 1) * n]), (roll, name, r)
+        for r in range(2):
+            assert torch.equal(bs[r].terminal_rows, bw.terminal_rows[r * n:(r + 1) * n]), (roll, r)
+            for name in ("ep_return", "ep_len", "livelock"):
+                assert torch.equal(getattr(shards[r], name), getattr(whole, name)[r * n:(r + 1) * n]), (roll, name)
+    whole.poll_error()
+    a = whole.dump_state()
+    tot = 0
+    for r in range(2):
+        shards[r].poll_error()
+        b = shards[r].dump_state()
+        for k in a:
+            assert np.array_equal(np.asarray(b[k]), np.asarray(a[k])[r * n:(r + 1) * n], equal_nan=True), (r, k)
+        tot += shards[r].stats()["resets"]
+    assert tot == whole.stats()["resets"]

@@ -82,3 +82,26 @@ def test_vec_env_subclasses_sb3_vecenv_when_importable():
     for m in ("reset", "step_async", "step_wait", "step", "seed", "close", "get_attr", "set_attr", "env_method",
               "env_is_wrapped", "get_images", "render"):
         assert callable(getattr(V.MgxVecEnv, m)), m
+
+
+def test_raw_direction_space_follows_make_env():
+    """environment.py:28-29: Discrete2BoxWrapper (one-hot Box(4,)) only when n_frames_stack > 1 and not
+    recurrent; otherwise MiniGridEnv's own Discrete(4)."""
+    box, _ = make_spaces(1, raw=True)
+    assert tuple(box["direction"].shape) == (4,)
+    disc, _ = make_spaces(1, raw=True, dir_one_hot=False)
+    assert disc["direction"].n == 4 and tuple(disc["direction"].shape) == ()
+
+
+def test_dummy_vec_env_semantics_warn():
+    """ppo.py:121 picks DummyVecEnv outside single-run mode; its envs share one process-global MT19937
+    stream, which the engine does not interleave: asking for it with n_envs > 1 warns (before the
+    engine, so this runs without a GPU too)."""
+    import pytest
+    with pytest.warns(RuntimeWarning, match="DummyVecEnv"):
+        try:
+            V.MgxVecEnv(4, vec_env_cls="dummy")
+        except Exception as e:                      # no GPU here: the engine itself refuses after the warning
+            assert "GPU" in str(e) or "device" in str(e).lower(), e
+    with pytest.raises(ValueError):
+        V.MgxVecEnv(4, vec_env_cls="forked")

@@ -159,3 +159,37 @@ def test_raw_mode_under_sb3_wrappers_matches_reference_stack(problem, mission, s
             assert _same_obs(i1[i]["terminal_observation"], i2[i]["terminal_observation"]), (t, i)
             assert i1[i]["episode"]["l"] == i2[i]["episode"]["l"], (t, i)
     raw.close()
+
+
+@pytest.mark.parametrize("n_frames_stack,recurrent", [(1, False), (4, True)])
+def test_raw_mode_direction_is_discrete_without_discrete2box(n_frames_stack, recurrent):
+    """make_env adds Discrete2BoxWrapper only when n_frames_stack > 1 and not recurrent
+    (environment.py:28-29): otherwise the raw env's direction is MiniGridEnv's Discrete(4), an int per
+    env -- obs and terminal_observation -- equal to the C oracle's agent direction."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import oracle as O
+    from mgx import MgxVecEnv
+    n, T = 128, 96
+    kw = dict(problem="multi", mission=None, size=8, num_objects=4, seed=42)
+    ref = O.OracleVec(n_envs=n, **kw)
+    env = MgxVecEnv(n, raw=True, n_frames_stack=n_frames_stack, recurrent=recurrent, **kw)
+    sp = env.observation_space["direction"]
+    assert getattr(sp, "n", None) == 4 and tuple(sp.shape) == ()
+    o = env.reset()
+    r = ref.reset()
+    assert o["direction"].shape == (n,) and o["direction"].dtype == np.int64
+    assert np.array_equal(o["direction"], r["dir"]) and np.array_equal(o["image"], r["image"])
+    rng = np.random.default_rng(31)
+    for t in range(T):
+        a = rng.integers(0, 7, n)
+        o, rew, d, infos = env.step(a)
+        w = ref.step(a.astype(np.int32))
+        done = (w["terminated"] | w["truncated"]).astype(bool)
+        assert np.array_equal(d, done), t
+        assert np.array_equal(o["direction"], np.where(done, w["r_dir"], w["dir"])), t
+        assert np.array_equal(o["image"], np.where(done[:, None, None, None], w["r_image"], w["image"])), t
+        for i in np.nonzero(done)[0]:
+            to = infos[i]["terminal_observation"]
+            assert int(to["direction"]) == int(w["dir"][i]) and np.array_equal(to["image"], w["image"][i]), (t, i)
+    env.close()
