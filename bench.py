@@ -340,6 +340,20 @@ def _ppo_success(pol, env_kw, episodes, dev):
             "seconds": round(time.perf_counter() - t0, 3)}
 
 
+def _rocprof_kernel_avg(path, kernel):
+    """Average duration (us) of `kernel` (name substring) in a rocprofv3 --stats kernel_stats.csv, or None."""
+    import csv
+    try:
+        rows = list(csv.DictReader(open(path)))
+    except OSError:
+        return None
+    for r in rows:
+        if kernel in r.get("Name", ""):
+            return {"avg_us": float(r["AverageNs"]) / 1e3, "calls": int(r["Calls"]),
+                    "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def pick_epoch(K, D=256):
     """Refill epoch E (mgx refill_every) so that the K timed steps are whole epochs: the largest
     divisor of K in [8, min(64, D/4)] (at D/2 the ring invariant 2E <= D makes every epoch refill the
@@ -434,7 +448,13 @@ def measure_rollout(args, layout, world, rank, dev):
     vals = torch.randn((H, n), device=dev, generator=g)
     last_v = torch.randn(n, device=dev, generator=g)
     adv, ret = torch.empty_like(rew), torch.empty_like(rew)
-    st = torch.zeros(3, dtype=torch.float64, device=dev)
+    nchunks = K // H
+    # the (sum A, sum A^2, n) triple of each horizon chunk is accumulated by GAE straight into its row of
+    # `hist` (which the N>1 all-reduce reads), through a shard scratch allocated here -- outside the
+    # captured graphs, so they hold neither a zero-fill nor a copy of the triple
+    hist = torch.zeros((nchunks, 3), dtype=torch.float64, device=dev)
+    from mgx import _lib as _L
+    scratch = torch.zeros(_L.GAE_SCRATCH_WORDS, dtype=torch.float64, device=dev)
     gamma, lam = 0.8108071290665859, 0.9452281119742252
     eng.reset()
     stream = torch.cuda.current_stream(dev)
@@ -456,7 +476,6 @@ def measure_rollout(args, layout, world, rank, dev):
     assert eng.calls % E == 0                            # the timed region starts on an epoch boundary
 
     def chunk(c):
-        st.zero_()
         if compact:
             if c:
                 cbuf.carry_over()
@@ -469,12 +488,11 @@ def measure_rollout(args, layout, world, rank, dev):
         else:
             for j in range(H):
                 eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
-        gae_dones(rew, vals, dones, last_v, gamma, lam, stats=st, out=(adv, ret))
+        gae_dones(rew, vals, dones, last_v, gamma, lam, stats=hist[c], scratch=scratch, out=(adv, ret))
         eng.join()                                       # the epoch's refill (it ran beside GAE): the
                                                          # chunk's graph is self-contained, and the region
                                                          # pays for every refill it forked
 
-    nchunks = K // H
     graphs = []
     forks0 = eng.stats()["refill_launches"]
     if args.graph:
@@ -498,7 +516,7 @@ def measure_rollout(args, layout, world, rank, dev):
     # refill launches inside the timed region: the forks the steps enqueued (captured once in the
     # graphs, replayed once each; eagerly, counted as they run)
     forks = (st0["refill_launches"] - forks0) if graphs else None
-    hist = torch.zeros((nchunks, 3), dtype=torch.float64, device=dev)
+    hist.zero_()                                         # (the untimed replays accumulated into it)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -511,7 +529,6 @@ def measure_rollout(args, layout, world, rank, dev):
             graphs[c].replay()
         else:
             chunk(c)
-        hist[c].copy_(st)
         if world > 1:                                    # the one exchange per rollout
             hist[c].copy_(_allreduce(hist[c], dist.ReduceOp.SUM))
     ev1.record(stream)
@@ -592,21 +609,31 @@ def measure_rollout(args, layout, world, rank, dev):
         b_alg = B_STEP * n + (3 * args.size ** 2 + 208) * resets_per_launch
         achieved = b_alg / per_launch_s / 1e9
         traffic, traffic_src = None, None
-        # rocprofv3 PMC HBM bytes of this kernel at this config (tools/gpu_r3_profiles.sh -> profiles/r03_pmc/)
+        # rocprofv3 PMC HBM bytes of this kernel at this config AND launch shape (a fused launch of E steps
+        # moves per step what E steps share: the PMC file must have steps_per_launch == E), committed under
+        # profiles/r04_pmc/ (tools/gpu_r4_profiles.sh), else an older round's matching file
         import glob
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r03_pmc", "pmc_[0-9]_%s.json" % layout)))
+        spl = E if fused else 1
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04_pmc", "pmc_[0-9]_%s*.json" % layout)))
+        cands += sorted(glob.glob(os.path.join(ROOT, "profiles", "r03_pmc", "pmc_[0-9]_%s.json" % layout)))
         cands += [PMC_FILE_FUSED if fused else (PMC_FILE_COMPACT if compact else PMC_FILE)]
         for pmc_file in cands:
             try:
                 pmc = json.load(open(pmc_file))
             except (OSError, ValueError):
                 continue
-            if pmc.get("n_envs") == n and pmc.get("size") == args.size and pmc.get("mission") == mission:
+            if (pmc.get("n_envs") == n and pmc.get("size") == args.size and pmc.get("mission") == mission
+                    and pmc.get("steps_per_launch", 1) == spl):
                 traffic = pmc.get("hbm_bytes_per_launch")
                 if traffic is not None:                  # per step (a fused launch holds several)
-                    traffic = traffic / pmc.get("steps_per_launch", 1)
+                    traffic = traffic / spl
                     traffic_src = os.path.relpath(pmc_file, ROOT)
                 break
+        # the same kernel's average duration from the committed rocprofv3 kernel stats of this exact command
+        # shape (profiles/r04_pmc/kernel_stats_<cfg>_<layout>_e<E>.csv): `frac` recomputed from profiles/
+        kstat = _rocprof_kernel_avg(os.path.join(ROOT, "profiles", "r04_pmc", "kernel_stats_%d_%s_e%d.csv" % (
+            args.config, layout, spl if fused else E)), "mgx_rollout_kernel" if fused else
+            ("mgx_step_kernel<int, true>" if compact else "mgx_step_kernel<int, false>"))
         # VecFrameStack image + direction roll (reported separately); the compact layout rolls nothing
         stack_bytes = 0 if compact else n * (441 + 588 + 12 + 16)
         out = {
@@ -649,6 +676,11 @@ def measure_rollout(args, layout, world, rank, dev):
                                     "mgx_step_kernel<int, true> (compact)" if compact else
                                     "mgx_step_kernel<int, false> (SB3 stacks)"),
                          "avg_launch_us": per_launch_s * 1e6,
+                         "rocprof": None if kstat is None else {
+                             "source": kstat["source"], "avg_launch_us": kstat["avg_us"] / spl,
+                             "frac": b_alg / (kstat["avg_us"] / spl * 1e-6) / 1e9 / PEAK_HBM_GBPS,
+                             "note": "the committed rocprofv3 --stats average of the same kernel at this config and "
+                                     "launch shape (per step), B_alg of this run"},
                          "probe_launches": len(probe_us),
                          "step_pipeline_us": float(gpu_ms) * 1e3 / K,
                          "alg_bytes_per_launch": b_alg, "resets_per_launch": resets_per_launch,

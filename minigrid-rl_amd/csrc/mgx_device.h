@@ -21,7 +21,13 @@
 // (see_through_walls=False -> apply_vis()) (3P),
 // CPython random (_randbelow via getrandbits) and numpy PCG64/Generator.integers (A.6).
 #pragma once
+#ifndef MGX_HOST_SIM
 #include <hip/hip_runtime.h>
+#else
+// tests/host_gen: the generator compiled for the host (one lane at a time) as a CPU check of its draw
+// order against the C oracle; the harness defines the few device intrinsics used here
+#include "host_sim.h"
+#endif
 #include <stdint.h>
 
 #include "mgx_diag.h"
@@ -171,6 +177,36 @@ __device__ __forceinline__ int pcg_integers(Pcg &p, int lo, int hi) {
         }
     }
     return lo + (int)(m >> 32);
+}
+
+// Two consecutive Generator.integers(0, S) draws (a position (x, y), S >= 2) with one PCG64 step and no
+// branch on the half-word buffer: the pair always consumes exactly one 64-bit output -- buffered low half
+// + the new output's low half (has = 1: the new high half is buffered), or the new output's two halves
+// (has = 0) -- so `has` is the same after the pair as before.  A Lemire rejection (probability S / 2^32 per
+// draw) replays the pair through pcg_integers from the saved state.  Same values and state as two
+// pcg_integers(p, 0, S) calls.
+__device__ __forceinline__ void pcg_cell(Pcg &p, int S, int &x, int &y) {
+    const Pcg p0 = p;
+    const uint64_t n = pcg_next64(p);
+    const uint32_t lo = (uint32_t)n, hi = (uint32_t)(n >> 32);
+    const uint32_t a = p.has ? p.uinteger : lo, b = p.has ? lo : hi;
+    p.uinteger = p.has ? hi : p.uinteger;
+    const uint32_t s = (uint32_t)S;
+    if ((s & (s - 1u)) == 0u) {                                   // power of two (S = 8, 16): top bits
+        const int k = 32 - __builtin_ctz(s);
+        x = (int)(a >> k);
+        y = (int)(b >> k);
+        return;
+    }
+    const uint64_t ma = (uint64_t)a * s, mb = (uint64_t)b * s;
+    if ((uint32_t)ma < s || (uint32_t)mb < s) {                  // Lemire's rejection test may apply: replay
+        p = p0;
+        x = pcg_integers(p, 0, S);
+        y = pcg_integers(p, 0, S);
+        return;
+    }
+    x = (int)(ma >> 32);
+    y = (int)(mb >> 32);
 }
 
 // numpy SeedSequence(seed).generate_state(4, uint64) -> PCG64 seeding.
@@ -347,7 +383,11 @@ __device__ __forceinline__ void put(Gen<NW> &G, int x, int y, uint8_t code) {   
 // independent 16-B global loads in flight (one L2/HBM round trip), 32 b64 LDS stores.
 // Out of line: it is the cold path of every draw site (inlined at each of them it
 // made the generator ~2k instructions larger).
+#ifndef MGX_HOST_SIM
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
+#else
+typedef uint64_t lds_u64;
+#endif
 constexpr int MT_PAD = MT_WG_MAX + 4;   // mirror pad groups after the ring (a window may start in its last slot)
 template <int WG>
 __device__ __noinline__ void mt_refill_cold(const uint64_t *__restrict__ table, uint64_t slot, lds_u64 *win) {
@@ -471,6 +511,47 @@ __device__ __forceinline__ void mt_advance(Gen<NW> &G, int m) {
         G.gc = win_group(G, G.gi + 2);
     }
 }
+// `cnt` (<= 12) successive _randbelow draws whose moduli are known up front -- draw i's modulus in bits
+// 5i..5i+4 of `prog`, its value returned in the same bits: the door draws of the room generators (colour,
+// locked, key-in-box per door, then the door positions, custom_env.py:635-650, 878-930, 1322-1391) and the
+// mission / room-count draws before them.  Each pass over the ten words of the register queue decodes as
+// many consecutive draws as it holds (draw i = the first word after draw i-1's that passes draw i's test,
+// one SWAR compare and a find-first-set each); a draw that finds no accepted word in the rest of the ten
+// consumes them all and continues in the next pass.  Word consumption and the live-lock cap are those of
+// cnt randbelow() calls, which spent a whole pass (and its group rotation) per draw (round 4).
+template <int NW>
+__device__ __forceinline__ uint64_t randbelow_seq(Gen<NW> &G, uint64_t prog, int cnt) {
+    constexpr uint64_t GM = 32ull * MT_REP;              // guard bit of every slot
+    uint64_t res = 0;
+    int i = 0;
+#pragma unroll 1
+    while (i < cnt) {
+        GCOUNT(G, 21);
+        const int o6 = (int)__umul24((uint32_t)G.go, 6u);
+        const uint64_t f = ((G.ga >> o6) | (G.gb << (60 - o6))) & MT_LOW60;   // words cur..cur+9
+        uint64_t avail = GM;                             // slots after the last decoded draw
+        int used = MT_FIELDS;                            // words this pass consumes
+#pragma unroll 1
+        while (i < cnt) {
+            const RbConst K = rb_const((uint32_t)(prog >> (5 * i)) & 31u);
+            const uint64_t acc = (K.c1 - f) & avail;
+            if (!acc) { used = MT_FIELDS; break; }       // draw i runs past these ten words
+            const int b = __ffsll((long long)acc) - 1;   // guard bit 6 j + 5 of the accepted word j
+            res |= (uint64_t)((((uint32_t)(f >> (b - 5))) & 31u) >> K.sh) << (5 * i);
+            avail &= ~((2ull << b) - 1ull);
+            used = (int)((uint32_t)(b + 1) * 171u >> 10);   // j + 1
+            i++;
+        }
+        const uint32_t left = G.llw - (uint32_t)(G.cur - G.astart);
+        if ((uint32_t)used > left) {                     // the cap comes before the sequence's end
+            G.cur = G.astart + G.llw;
+            G.abort = true;
+            return res;
+        }
+        mt_advance(G, used);
+    }
+    return res;
+}
 // The reference's rejection loop `while True: x = randint(x0, x1); y = randint(y0, y1);
 // if ok(x, y): break` (two _randbelow per draw) with the rejected cells as a bit set.  One SWAR
 // pass over the next ten words finds every complete draw they hold: x is the first word passing
@@ -478,19 +559,43 @@ __device__ __forceinline__ void mt_advance(Gen<NW> &G, int m) {
 // draw costs a few bit operations instead of two randbelow calls.  A draw that straddles the
 // ten words is taken word by word (randbelow_c).  Word consumption and the live-lock cap are
 // exactly randbelow's: the attempt is abandoned when a draw would need a word past the cap.
+// has_c: the draw is preceded by one more _randbelow (modulus KC: an object placement's
+// random.choice(obj_choice), custom_env.py:662-667 -- no MT word is drawn between the two), decoded from
+// the first pass's words before the cell candidates (round 4: it took a randbelow pass of its own) ->
+// `choice`.
 template <int NW, typename Bad, typename Sat>
 __device__ __forceinline__ void draw_cell(Gen<NW> &G, const RbConst KX, const RbConst KY, int x0, int y0, int &x, int &y,
-                                          Bad bad, Sat sat /* probe after SAT_PROBE rejections; null: none */) {
+                                          Bad bad, Sat sat /* probe after SAT_PROBE rejections; null: none */,
+                                          bool has_c, const RbConst KC, int &choice) {
     constexpr uint64_t GM = 32ull * MT_REP;              // guard bit of every slot
     int rej = 0;
+    bool need_c = has_c;
 #pragma unroll 1
     for (;;) {
         GCOUNT(G, 21);
         const int o6 = (int)__umul24((uint32_t)G.go, 6u);
         const uint64_t f = ((G.ga >> o6) | (G.gb << (60 - o6))) & MT_LOW60;   // words cur..cur+9
+        uint64_t avail = GM;                             // slots not consumed by an earlier draw
+        int used = 0;                                    // words through the last draw examined
+        if (need_c) {
+            const uint64_t acc = (KC.c1 - f) & GM;
+            if (!acc) {                                  // the choice runs past these ten words
+                const uint32_t left = G.llw - (uint32_t)(G.cur - G.astart);
+                if ((uint32_t)MT_FIELDS > left) {
+                    G.cur = G.astart + G.llw;
+                    G.abort = true;
+                    return;
+                }
+                mt_advance(G, MT_FIELDS);
+                continue;
+            }
+            const int b = __ffsll((long long)acc) - 1;
+            choice = (int)((((uint32_t)(f >> (b - 5))) & 31u) >> KC.sh);
+            avail &= ~((2ull << b) - 1ull);
+            used = (int)((uint32_t)(b + 1) * 171u >> 10);
+            need_c = false;
+        }
         const uint64_t accx = (KX.c1 - f) & GM, accy = (KY.c1 - f) & GM;    // slot passes x's / y's test
-        uint64_t avail = GM;                             // slots not consumed by an earlier candidate
-        int used = 0;                                    // words through the last candidate examined
         bool ok = false;
 #pragma unroll 1
         for (;;) {
@@ -565,8 +670,8 @@ __device__ __forceinline__ void draw_free_cell(Gen<NW> &G, int &px, int &py) {
     for (uint32_t it = 0;; ++it) {
         GCOUNT(G, 22);
         if (it > PCG_LOOP_LIMIT) { G.err |= 4u; px = 1; py = 1; return; }
-        const int x = pcg_integers(G.pcg, 0, G.S);
-        const int y = pcg_integers(G.pcg, 0, G.S);
+        int x, y;
+        pcg_cell(G.pcg, G.S, x, y);
         if (occupied(G, y * G.S + x)) continue;
         if (x == G.ax && y == G.ay) continue;
         px = x; py = y;
@@ -787,30 +892,54 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     if (nr == 3) for (int i = 1; i < mid; i++) put(G, i, mid, CODE_WALL);
     if (nr == 4) for (int i = 1; i < S - 1; i++) put(G, i, mid, CODE_WALL);
     const int ndoors = nr == 2 ? 1 : nr;
+    const bool ado = G.all_doors_open;
     uint32_t oc = 0x3FFFFu;    // obj_choice: bit = type_slot*6 + colour-name (key, ball, box)
     uint32_t dc = 0x3Fu;       // door_colors
     uint32_t dinfo = 0;        // per door byte: colour | locked<<3 | key_in_box<<4
-    // colour / locked / key_in_box draws, door by door (custom_env.py:635-643, 878-908, 1322-1362)
+    // colour / locked / key_in_box draws, door by door (custom_env.py:635-643, 878-908, 1322-1362):
+    // random.choice(door_colors) of the 6 - d colours left = randbelow(6 - d), locked = choice([True, False])
+    // = randbelow(2) == 0 (not drawn when all_doors_open), key_in_box likewise -- one fixed sequence
+    uint64_t prog = 0;
+    int cnt = 0;
 #pragma unroll 1
     for (int d = 0; d < ndoors; d++) {
-        const int col = mask_choice(G, dc);
+        prog |= (uint64_t)(6 - d) << (5 * cnt++);
+        if (!ado) prog |= 2ull << (5 * cnt++);
+        prog |= 2ull << (5 * cnt++);
+    }
+    const uint64_t dr = randbelow_seq(G, prog, cnt);
+    if (G.abort) return;
+#pragma unroll 1
+    for (int d = 0, k = 0; d < ndoors; d++) {
+        const int col = nth_set_bit(dc, (int)(dr >> (5 * k++)) & 31);
         dc &= ~(1u << col);
-        const bool lk = G.all_doors_open ? false : choice_bool(G);
-        const bool kib = choice_bool(G);
+        const bool lk = ado ? false : ((dr >> (5 * k++)) & 31) == 0;
+        const bool kib = ((dr >> (5 * k++)) & 31) == 0;
         if (lk) { oc &= ~(1u << col); if (kib) oc &= ~(1u << (12 + col)); }
         dinfo |= (uint32_t)(col | (lk << 3) | (kib << 4)) << (8 * d);
     }
     GSTAMP(G, 11);                                               // walls + door colour/lock draws
-    if (G.abort) return;
-    // door positions (custom_env.py:646-650, 911-930, 1365-1391)
+    // door positions (custom_env.py:646-650, 911-930, 1365-1391): randint(lo, hi) = lo + randbelow(hi - lo + 1)
+    // per door [+ is_open = choice([True, False]) when all_doors_open], again one sequence
+    prog = 0;
+    cnt = 0;
 #pragma unroll 1
-    for (int d = 0; d < ((MGX_GEN_SKIP & 2) ? 0 : ndoors); d++) {
+    for (int d = 0; d < ndoors; d++) {
         bool horiz; int lo, hi;
         door_geom(nr, d, mid, S, horiz, lo, hi);
-        const int v = randint(G, lo, hi);
+        prog |= (uint64_t)(hi - lo + 1) << (5 * cnt++);
+        if (ado) prog |= 2ull << (5 * cnt++);
+    }
+    const uint64_t pr = randbelow_seq(G, prog, (MGX_GEN_SKIP & 2) ? 0 : cnt);
+    if (G.abort) return;
+#pragma unroll 1
+    for (int d = 0, k = 0; d < ((MGX_GEN_SKIP & 2) ? 0 : ndoors); d++) {
+        bool horiz; int lo, hi;
+        door_geom(nr, d, mid, S, horiz, lo, hi);
+        const int v = lo + (int)((pr >> (5 * k++)) & 31);
         const int x = horiz ? v : mid, y = horiz ? mid : v;
         const uint32_t di = dinfo >> (8 * d);
-        const bool open = G.all_doors_open ? choice_bool(G) : false;
+        const bool open = ado ? ((pr >> (5 * k++)) & 31) == 0 : false;
         put_door(G, x, y, (uint8_t)door_code(di & 7, (di >> 3) & 1, open));
         add_obj(G, T_DOOR, di & 7, x, y);
     }
@@ -830,8 +959,8 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
         for (uint32_t it = 0;; ++it) {
             GCOUNT(G, 22);
             if (it > 2 * PCG_LOOP_LIMIT) { G.err |= 4u; G.ax = 1; G.ay = 1; break; }
-            const int x = pcg_integers(G.pcg, 0, S);
-            const int y = pcg_integers(G.pcg, 0, S);
+            int x, y;
+            pcg_cell(G.pcg, S, x, y);
             if (occupied(G, y * S + x)) continue;          // (the agent is not placed yet: G.ax = -1)
             if (agent) { G.ax = x; G.ay = y; break; }
             if (next2door(G, x, y)) continue;              // goal placed then removed: net no-op
@@ -915,12 +1044,12 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
             if (phase == 1 && ((keymask >> (2 * r)) & 1)) { ox = kx; oy = ky; }   // key A came just before
         } else {
             if (oc == 0) { G.err |= 8u; break; }
-            const int b = (MGX_GEN_SKIP & 32) ? __ffs(oc) - 1 : mask_choice(G, oc);
-            if (G.abort) return;
-            oc &= ~(1u << b);
-            ot = MULTI_TYPES[b / 6];
-            cname = b % 6;
+            // the object's random.choice(obj_choice) is the first draw of its placement's rejection loop's
+            // first pass (draw_cell has_c); the type and colour are taken once the cell is drawn
         }
+        const bool has_c = !is_key && !(MGX_GEN_SKIP & 32);
+        const RbConst kc_ = rb_const(is_key ? 1u : (uint32_t)__popc(oc));
+        int choice = 0;
         // cells this placement rejects: key -> goal, [agent], [the other key], next to a door;
         // object -> occupied, agent, next to a door
         const int ex0 = is_key ? gx : G.ax, ey0 = is_key ? gy : G.ay;
@@ -943,9 +1072,14 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
             } else {
                 sat = rect_has_free(G, x0, x1, y0, y1, !is_key, ex0, ey0, ex1, ey1, ox, oy);
             }
-            if (!sat) { live_lock(G); return; }
+            if (!sat) {
+                // no acceptable cell: the reference's loop never ends -> live-lock policy at once (the choice
+                // draw before it changes nothing: the attempt's cursor jumps to its cap either way)
+                live_lock(G);
+                return;
+            }
             draw_cell(G, kx_, ky_, x0, y0, x, y, [&](int cx, int cy) { return bad.test(cy * S + cx); },
-                      [] { return true; });
+                      [] { return true; }, has_c, kc_, choice);
             if (G.abort) return;
         } else {
             // S > 11: the cells are tested in the LDS grid; after SAT_PROBE rejections an exhaustive
@@ -959,8 +1093,14 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
                     for (int yy = y0; yy <= y1; yy++)
                         if (!bad(xx, yy)) return true;
                 return false;
-            });
+            }, has_c, kc_, choice);
             if (G.abort) return;
+        }
+        if (!is_key) {                                           // commit the object's type and colour
+            const int b = (MGX_GEN_SKIP & 32) ? __ffs(oc) - 1 : nth_set_bit(oc, choice);
+            oc &= ~(1u << b);
+            ot = MULTI_TYPES[b / 6];
+            cname = b % 6;
         }
         GSTAMP(G, 18);                                           // inner rejection loop
         // commit the placement, then the next task
@@ -976,15 +1116,13 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
 
 template <int NW>
 __device__ __forceinline__ int gen_multi(Gen<NW> &G) {             // custom_env.py:595-615
-    int cmd;
-    if (G.cfg_mission >= 0) cmd = G.cfg_mission;
-    else {
-        const int r = randbelow(G, 4);                               // choice([0, 1, 2, 5])
-        cmd = r == 3 ? 5 : r;
-    }
+    // [choice([0, 1, 2, 5]) = randbelow(4) when the config names no mission] then randint(2, 4)
+    const bool draw_cmd = G.cfg_mission < 0;
+    const uint64_t r = randbelow_seq(G, draw_cmd ? (4ull | (3ull << 5)) : 3ull, draw_cmd ? 2 : 1);
     if (G.abort) return 0;
-    const int nr = randint(G, 2, 4);
-    if (G.abort) return 0;
+    const int rc = (int)(r & 31);
+    const int cmd = draw_cmd ? (rc == 3 ? 5 : rc) : G.cfg_mission;
+    const int nr = 2 + (int)((draw_cmd ? r >> 5 : r) & 31);
     GSTAMP(G, 10);                                               // mission + room-count draws
     gen_rooms(G, nr);
     return cmd;

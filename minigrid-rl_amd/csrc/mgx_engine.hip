@@ -2724,7 +2724,10 @@ static mgx_status join_refill(mgx_handle *h, void *stream) {
 // Epoch start: join the last refill (and the slide after it, which published its tails in ring_pubn),
 // then fork this epoch's refill onto the side stream.  It writes only slots the steps cannot pop before
 // the next publish, and RNG state only the refill uses.
-static mgx_status fork_refill(mgx_handle *h, void *stream) {
+// In two halves so that a caller can enqueue its own launch between them: fork_begin joins the previous
+// epoch's refill and records the fork point on `stream`; fork_end launches this epoch's refill on the side
+// stream from that point.  Whatever is launched on `stream` in between runs beside the refill, not after it.
+static mgx_status fork_begin(mgx_handle *h, void *stream) {
     // the previous epoch's refill is joined here, not at that epoch's last step: work the caller
     // enqueues between epochs (GAE, the policy forward) runs beside the refill's tail.  No copy on this
     // stream: the fused rollout reads ring_pubn, the per-step calls copy it to ring_pub at their first
@@ -2734,11 +2737,19 @@ static mgx_status fork_refill(mgx_handle *h, void *stream) {
     h->pub_stale = true;
     if (h->serial_refill) return launch_refill(h, stream);
     HIP_TRY(hipEventRecord(h->ev_fork, (hipStream_t)stream));
+    return MGX_OK;
+}
+static mgx_status fork_end(mgx_handle *h) {
+    if (h->serial_refill) return MGX_OK;
     HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
     mgx_status s = launch_refill(h, h->side, h->ev_done);
     if (s != MGX_OK) return s;
     h->in_flight = true;
     return MGX_OK;
+}
+static mgx_status fork_refill(mgx_handle *h, void *stream) {
+    mgx_status s = fork_begin(h, stream);
+    return s != MGX_OK ? s : fork_end(h);
 }
 
 // mgx_step_kernel pops below ring_pub, which must not move within a launch (its waves read it
@@ -2925,8 +2936,13 @@ mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K,
     o.ep_ret = out->ep_return_dev;
     o.ep_len = out->ep_len_dev;
     o.livelock = out->livelock_dev;
-    if (h->calls % E == 0) {
-        mgx_status fs = fork_refill(h, stream);
+    // The rollout is launched BEFORE the epoch's refill is (both start from the same fork point): its
+    // workgroups take their CU slots first and the refill's waves fill the rest, in eager streams and in a
+    // captured hipGraph alike.  (With the refill enqueued first, a graph replay dispatched the refill's 1,024
+    // waves first and the 20-step rollout took 181 instead of 133 us: tools/trace_epochs.py, round 4.)
+    const bool fork = h->calls % E == 0;
+    if (fork) {
+        mgx_status fs = fork_begin(h, stream);
         if (fs != MGX_OK) return fs;
     }
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
@@ -2937,6 +2953,10 @@ mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K,
         hipLaunchKernelGGL(mgx_rollout_kernel<false>, dim3((unsigned)nblk), dim3(ROLL_THREADS), h->lds_rollout,
                            (hipStream_t)stream, h->kp, o, actions_dev, K);
     HIP_TRY(hipGetLastError());
+    if (fork) {
+        mgx_status fs = fork_end(h);
+        if (fs != MGX_OK) return fs;
+    }
     h->calls += (uint64_t)K;
     return MGX_OK;
 }

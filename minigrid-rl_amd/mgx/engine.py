@@ -206,6 +206,14 @@ class MgxEngine:
             pass
 
 
+def _scratch_for(stats, scratch):
+    if scratch is None:
+        return _stats_scratch(stats)
+    assert stats is not None and scratch.dtype == torch.float64 and scratch.is_contiguous() \
+        and scratch.numel() >= _lib.GAE_SCRATCH_WORDS and scratch.device == stats.device
+    return scratch
+
+
 def _stats_scratch(stats):
     """The adv-stat shard scratch (include/mgx.h, MGX_GAE_SCRATCH_WORDS) of this `stats` tensor on the
     calling stream: GAE calls on different streams (e.g. two collectors) never share partial sums; calls on
@@ -223,12 +231,13 @@ def _stats_scratch(stats):
     return buf
 
 
-def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lambda, stats=None):
+def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lambda, stats=None, scratch=None):
     """DictRolloutBuffer.compute_returns_and_advantage on device (libmgx mgx_gae).
 
     rewards/values/episode_starts: f32 [T, N]; last_values f32 [N]; last_dones bool/u8 [N].
     Returns (advantages, returns) f32 [T, N].  `stats` (f64 [3] tensor, optional)
-    accumulates (sum A, sum A^2, count)."""
+    accumulates (sum A, sum A^2, count); `scratch` (f64 [MGX_GAE_SCRATCH_WORDS], zeroed, optional) the
+    caller's shard partials (default: one per stats tensor and stream)."""
     L = _lib.load()
     T, N = rewards.shape
     for t in (rewards, values, episode_starts):
@@ -241,11 +250,11 @@ def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lam
     stream = ctypes.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
     _lib.check(L.mgx_gae(_ptr(rewards), _ptr(values), _ptr(episode_starts), _ptr(lv), _ptr(ld), T, N,
                          ctypes.c_float(gamma), ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats),
-                         _ptr(_stats_scratch(stats)), stream), "mgx_gae")
+                         _ptr(_scratch_for(stats, scratch)), stream), "mgx_gae")
     return adv, ret
 
 
-def gae_dones(rewards, values, dones, last_values, gamma, gae_lambda, stats=None, out=None):
+def gae_dones(rewards, values, dones, last_values, gamma, gae_lambda, stats=None, out=None, scratch=None):
     """GAE over the compact rollout layout (libmgx mgx_gae_dones): dones u8/bool [T, N] is
     the `done` of step t, i.e. SB3's episode_starts shifted by one plus last_dones.
     Returns (advantages, returns) f32 [T, N] (written into `out` if given)."""
@@ -259,6 +268,6 @@ def gae_dones(rewards, values, dones, last_values, gamma, gae_lambda, stats=None
     gl = float(torch.tensor(gamma * gae_lambda, dtype=torch.float64).float())
     stream = ctypes.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
     _lib.check(L.mgx_gae_dones(_ptr(rewards), _ptr(values), _ptr(dones), _ptr(lv), T, N, ctypes.c_float(gamma),
-                               ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats), _ptr(_stats_scratch(stats)),
+                               ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats), _ptr(_scratch_for(stats, scratch)),
                                stream), "mgx_gae_dones")
     return adv, ret

@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--lr0", type=float, default=1e-3)        # README.md:19-51 first-stage schedule (pkp0)
     ap.add_argument("--lr1", type=float, default=3e-5)
-    ap.add_argument("--mission", type=int, default=2)
+    ap.add_argument("--mission", default="2", help="2 PKP, 5 GTG, 0 GTO, 1 TGL, None = ALL (the mixed-task config 4)")
     ap.add_argument("--size", type=int, default=8)
     ap.add_argument("--eval-episodes", type=int, default=1000)
     ap.add_argument("--out", default=None)
@@ -58,7 +58,8 @@ def main():
     ap.add_argument("--progress", default=None, help="append one JSON line per rollout here")
     args = ap.parse_args()
     from mgx.ppo import PPOConfig, learn
-    env_kw = dict(problem="multi", mission=args.mission, size=args.size, num_objects=4)
+    mission = None if args.mission == "None" else int(args.mission)
+    env_kw = dict(problem="multi", mission=mission, size=args.size, num_objects=4)
     cfg = PPOConfig(n_envs=args.n_envs, horizon=args.horizon, batch_size=args.batch_size, n_epochs=args.epochs,
                     initial_learning_rate=args.lr0, final_learning_rate=args.lr1, env=env_kw)
     t0 = time.perf_counter()
@@ -82,9 +83,13 @@ def main():
     train_s = time.perf_counter() - t0
     eng.close()
     ev = success_rate(pol, env_kw, args.eval_episodes, seed=4242)
+    names = {2: "PKP", 5: "GTG", 0: "GTO", 1: "TGL", None: "ALL"}
+    # README.md:54-65's table: the model evaluated on every task (columns GTG GTO PKP TGL ALL)
+    per_task = {names[m]: success_rate(pol, dict(env_kw, mission=m), args.eval_episodes, seed=4242)
+                for m in (5, 0, 2, 1, None)} if mission is None else None
     out = {"what": "PPO (mgx.ppo.learn) on %s, then evaluate_policy over %d deterministic episodes on a fresh "
-                   "engine (seed 4242)" % ("PKP" if args.mission == 2 else "mission %d" % args.mission,
-                                           args.eval_episodes),
+                   "engine (seed 4242)" % (names.get(mission, "mission %s" % mission), args.eval_episodes),
+           "eval_per_task": per_task,
            "config": {"env": env_kw, "n_envs": cfg.n_envs, "horizon": cfg.horizon, "batch_size": cfg.batch_size,
                       "n_epochs": cfg.n_epochs, "optimizer_steps_per_rollout": cfg.n_epochs * cfg.n_envs *
                       cfg.horizon // cfg.batch_size, "lr": [cfg.initial_learning_rate, cfg.final_learning_rate],
@@ -93,7 +98,10 @@ def main():
            "timesteps": hist[-1]["timesteps"] if hist else 0, "rollouts": len(hist), "train_seconds": train_s,
            "env_steps_per_s_incl_training": (hist[-1]["timesteps"] / train_s) if hist else None,
            "eval": ev, "eval_random_policy": random_eval,
-           "reference": "README.md:61 PPO PKP model on PKP: 57% (1k episodes; size and training steps unstated)",
+           "reference": ("README.md:65 PPO ALL model: GTG 75%, GTO 65%, PKP 59%, TGL 58%, ALL 65% (1k episodes; trained "
+                         "through the all0..all6 curriculum, README.md:40-46; size and training steps unstated)"
+                         if mission is None else
+                         "README.md:61 PPO PKP model on PKP: 57% (1k episodes; size and training steps unstated)"),
            "curve": curve[::max(1, len(curve) // 40)]}
     print(json.dumps(out))
     if args.out:
