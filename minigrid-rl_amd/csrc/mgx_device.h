@@ -182,7 +182,8 @@ __device__ __forceinline__ int pcg_integers(Pcg &p, int lo, int hi) {
 // Two consecutive Generator.integers(0, S) draws (a position (x, y), S >= 2) with one PCG64 step and no
 // branch on the half-word buffer: the pair always consumes exactly one 64-bit output -- buffered low half
 // + the new output's low half (has = 1: the new high half is buffered), or the new output's two halves
-// (has = 0) -- so `has` is the same after the pair as before.  A Lemire rejection (probability S / 2^32 per
+// (has = 0; the high half stays in `uinteger`, as the second next32 leaves it) -- so `has` is the same after
+// the pair as before.  A Lemire rejection (probability S / 2^32 per
 // draw) replays the pair through pcg_integers from the saved state.  Same values and state as two
 // pcg_integers(p, 0, S) calls.
 __device__ __forceinline__ void pcg_cell(Pcg &p, int S, int &x, int &y) {
@@ -190,7 +191,7 @@ __device__ __forceinline__ void pcg_cell(Pcg &p, int S, int &x, int &y) {
     const uint64_t n = pcg_next64(p);
     const uint32_t lo = (uint32_t)n, hi = (uint32_t)(n >> 32);
     const uint32_t a = p.has ? p.uinteger : lo, b = p.has ? lo : hi;
-    p.uinteger = p.has ? hi : p.uinteger;
+    p.uinteger = hi;                  // has = 1: the new buffer; has = 0: the (dead) copy next32 leaves behind
     const uint32_t s = (uint32_t)S;
     if ((s & (s - 1u)) == 0u) {                                   // power of two (S = 8, 16): top bits
         const int k = 32 - __builtin_ctz(s);
@@ -266,7 +267,7 @@ constexpr int MT_FIELDS = 10;       // words per packed group
 // refill wave's LDS (13 KB) then fits four to a CU beside four rollout workgroups; 16 for larger grids
 // (their LDS budget is set by the grids; the window reloads half as often).
 template <int NW>
-__host__ __device__ constexpr int mt_wg() { return NW == 1 ? 8 : 16; }
+__host__ __device__ constexpr int mt_wg() { return NW == 1 ? MGX_MT_WG1 : 16; }
 constexpr int MT_WG_MAX = 16;
 template <int NW>   // dwords per lane window row: 8-B aligned, 2-way banked for b64
 __host__ __device__ constexpr int win_stride() { return 2 * mt_wg<NW>() + 2; }
@@ -334,6 +335,7 @@ struct Gen {
     uint32_t err;
     Pcg pcg;
     int ax, ay, adir;
+    int goalx, goaly;      // the first Goal added to objs (-1: none): the 'go to goal' target without a scan
     uint32_t *objs;        // LDS objs list: type | cname<<4 | x<<8 | y<<16 (cname 15 = None)
     int nobjs;
     uint32_t tmask;        // bit t: an object of type t is in objs
@@ -659,6 +661,9 @@ __device__ __forceinline__ void add_obj(Gen<NW> &G, int t, int cname, int x, int
     const bool full = G.nobjs >= MAX_OBJS;
     G.err |= full ? 8u : 0u;
     G.tmask |= full ? 0u : 1u << t;
+    const bool first_goal = !full && t == T_GOAL && G.goalx < 0;
+    G.goalx = first_goal ? x : G.goalx;
+    G.goaly = first_goal ? y : G.goaly;
     if (!full)
         G.objs[G.nobjs++] = (uint32_t)t | ((uint32_t)(cname & 15) << 4) | ((uint32_t)x << 8) | ((uint32_t)y << 16) | flags;
 }
@@ -1319,20 +1324,36 @@ __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
     const int S = G.S;
     {   // Grid(W, H) of None + wall_rect(0, 0, W, H); the row is 4-B aligned in LDS
         uint32_t *g32 = reinterpret_cast<uint32_t *>(G.g);
-        const int nw = (S * S + 3) >> 2;
-        for (int i = 0; i < nw; i++) g32[i] = 0x01010101u * CODE_EMPTY;
-        for (int i = 0; i < S; i++) {
-            G.g[i] = CODE_WALL; G.g[(S - 1) * S + i] = CODE_WALL;
-            G.g[i * S] = CODE_WALL; G.g[i * S + S - 1] = CODE_WALL;
+        if (NW == 1 && S == 8) {                                  // two dwords per row: 16 constant stores
+            constexpr uint32_t W4 = 0x01010101u * CODE_WALL;
+            constexpr uint32_t L4 = 0x01010100u * CODE_EMPTY | CODE_WALL, R4 = 0x00010101u * CODE_EMPTY | (uint32_t)CODE_WALL << 24;
+            g32[0] = W4; g32[1] = W4; g32[14] = W4; g32[15] = W4;
+#pragma unroll
+            for (int r = 1; r < 7; r++) { g32[2 * r] = L4; g32[2 * r + 1] = R4; }
+        } else {
+            const int nw = (S * S + 3) >> 2;
+            for (int i = 0; i < nw; i++) g32[i] = 0x01010101u * CODE_EMPTY;
+            for (int i = 0; i < S; i++) {
+                G.g[i] = CODE_WALL; G.g[(S - 1) * S + i] = CODE_WALL;
+                G.g[i * S] = CODE_WALL; G.g[i * S + S - 1] = CODE_WALL;
+            }
         }
     }
     G.occ.clear();                                                // wall_rect(0, 0, W, H)
-    for (int i = 0; i < S; i++) {
-        G.occ.set(i); G.occ.set((S - 1) * S + i);
-        G.occ.set(i * S); G.occ.set(i * S + S - 1);
+    if constexpr (NW == 1) {                                      // the border as one mask
+        const uint64_t row = (1ull << S) - 1ull;
+        uint64_t col = 0;
+        for (int i = 0; i < S; i++) col |= 1ull << (i * S);
+        G.occ.w0 = row | (row << ((S - 1) * S)) | col | (col << (S - 1));
+    } else {
+        for (int i = 0; i < S; i++) {
+            G.occ.set(i); G.occ.set((S - 1) * S + i);
+            G.occ.set(i * S); G.occ.set(i * S + S - 1);
+        }
     }
     G.dn.clear();
     G.ax = -1; G.ay = -1; G.adir = 0; G.nobjs = 0; G.tmask = 0;
+    G.goalx = -1; G.goaly = -1;
     GSTAMP(G, 9);                                                 // attempt setup (mt_sync, grid clear)
     int cmd;
     if constexpr (MULTI) cmd = gen_multi(G);
@@ -1377,9 +1398,9 @@ __device__ __forceinline__ void gen_attempt(Gen<NW> &G, ResetOut &R) {
         tx = (o >> 8) & 0xFF; ty = (o >> 16) & 0xFF;
         ta = cmd == 1 ? A_TOGGLE : A_PICKUP;
         mid = (cmd == 1 ? CMD_TOGGLE : CMD_PICKUP) | (((o >> 4) & 15) << 2) | (type_slot(o & 15) << 5);
-    } else {                                                      // 'go to goal'
-        for (int k = 0; k < G.nobjs; k++)
-            if ((G.objs[k] & 15) == T_GOAL) { tx = (G.objs[k] >> 8) & 0xFF; ty = (G.objs[k] >> 16) & 0xFF; break; }
+    } else if (G.goalx >= 0) {                                    // 'go to goal': the first Goal in objs
+        tx = (uint32_t)G.goalx;                                   // (recorded by add_obj: no scan of the list)
+        ty = (uint32_t)G.goaly;
     }
     R.tx = (uint8_t)tx; R.ty = (uint8_t)ty; R.ta = (uint8_t)ta; R.mission_id = (uint8_t)mid;
     R.range = range;

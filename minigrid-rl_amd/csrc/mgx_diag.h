@@ -42,6 +42,9 @@
 #ifndef MGX_MT_TOPUP        // wave-uniform MT window top-up at this many groups left (0: each lane reloads its
 #define MGX_MT_TOPUP 0      // window when it runs out)
 #endif
+#ifndef MGX_MT_WG1          // MT window groups per refill lane at S <= 8 (8 or 16; 16 for larger grids)
+#define MGX_MT_WG1 8
+#endif
 #ifndef MGX_SERIAL_REFILL   // refill on the caller's stream (the refill alone, for timing it)
 #define MGX_SERIAL_REFILL 0
 #endif

@@ -1177,7 +1177,12 @@ struct ROut {
 constexpr int ROLL_THREADS = BLOCK_THREADS + 64;
 
 
-template <bool VIS>   // see_through_walls == False (Grid.process_vis): its code only in the variant that needs it
+// Template flags keep what a config does not use out of the step loop (round 4: the loop held ~100 uniform
+// values -- output pointers, feature flags, LDS bases -- and spilled 65 SGPRs to VGPR lanes, ~86 v_readlane per
+// step): VIS see_through_walls == False (Grid.process_vis), MOVE 'move' missions (problems mov / full: target
+// ranges), R64 the optional f64 rewards.  ep_return / ep_len / livelock (after the last step only) are kept in
+// LDS and written after the loop.
+template <bool VIS, bool MOVE, bool R64>
 __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p, ROut o, const int32_t *__restrict__ actions,
                                                                       int K) {
     extern __shared__ __align__(16) uint8_t smem[];
@@ -1205,6 +1210,8 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     __shared__ rpos_t s_head[BLOCK_ENVS], s_pub[BLOCK_ENVS];
     __shared__ unsigned long long s_cnt[2];      // resets, abandoned attempts
     __shared__ uint32_t s_err;
+    __shared__ float s_lrew[BLOCK_ENVS];         // the last step's reward, step count, abandoned attempts
+    __shared__ int s_lsc[BLOCK_ENVS], s_lll[BLOCK_ENVS];
 
     const int tid = threadIdx.x, lane = tid & (BLOCK_ENVS - 1);
     const int64_t e0 = (int64_t)blockIdx.x * BLOCK_ENVS;
@@ -1217,7 +1224,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     if (wave0) {
         s_st[lane] = reinterpret_cast<const uint4 *>(p.state)[e0 + lc];
         s_head[lane] = p.ring_head[e0 + lc];
-        if (p.has_move) s_mr[lane] = p.range_cur[e0 + lc];
+        if (MOVE) s_mr[lane] = p.range_cur[e0 + lc];
         s_nh[1][lane] = NO_POP;
         if (lane < 2) s_cnt[lane] = 0;
         if (lane == 0) s_err = 0;
@@ -1271,16 +1278,16 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
 #else
 #define RSTAMP(k) do { } while (0)
 #endif
-    for (int t = 0; t < K; t++) {
-        const int tb = t & 1;
-        RSTAMP(0);
-        // thread index through an opaque copy: lane- / env-derived addresses are then computed inside
-        // each region of the step, instead of being hoisted out of the loop and kept live through all of
-        // them (96 -> fewer VGPRs; the render's and the step logic's registers no longer add up)
-        int tidv = tid;
-        asm volatile("" : "+v"(tidv));
-        const int lanev = tidv & (BLOCK_ENVS - 1);
-        if (dmaw) {
+    if (dmaw) {
+        // ---- the DMA wave's own loop (round 4: the waves' loops are separate, so that the values only one
+        // of them uses are not live across the other's: the single loop spilled 56-65 SGPRs).  Its barriers
+        // match the compute waves' one for one: A, the terminal-row barriers when s_tmask (block-uniform),
+        // process_vis's two, B.
+        for (int t = 0; t < K; t++) {
+            const int tb = t & 1;
+            int tidv = tid;
+            asm volatile("" : "+v"(tidv));
+            const int lanev = tidv & (BLOCK_ENVS - 1);
             // the next step's actions; the ring episode after next of every env that popped last step
             // (LDS-DMA only: a register load here would make the wave wait for it -- and for every
             // prefetch in flight -- before the post-logic barrier, the whole block with it)
@@ -1291,139 +1298,162 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 const uint32_t nh = s_nh[tb ^ 1][lanev];
                 if (nh != NO_POP && (rpos_t)(s_pub[lanev] - nh) > 1) stage((rpos_t)(nh + 1));
             }
-        } else if (wave0) {
-            // ---- the step: one lanev per env
-            bool tw = false;
-            uint8_t popb = 0xFF;
-            uint32_t nh = NO_POP;
-            if (lanev < ne) {
-                const uint32_t e = (uint32_t)(e0 + lanev), oi = (uint32_t)t * (uint32_t)N + e;   // N * K < 2^32
-                EnvState st;
-                {
-                    const uint4 sv = s_st[lanev];
-                    __builtin_memcpy(&st, &sv, sizeof st);
-                }
-                rpos_t rhead = s_head[lanev];
-                uint64_t mrange = p.has_move ? s_mr[lanev] : 0ull;
-                uint32_t err = 0;
-                int a = s_act[tb * BLOCK_ENVS + lanev];
-                if ((unsigned)a > 6u) { err |= MGX_DEVERR_BAD_ACTION; a = -1; }
-                const StepRes r = env_step(st, a, s_grid, lanev, S, p.manual, mrange);
-                tw = r.done && (p.terminal_mode == MGX_TERMINAL_ALL ||
-                                (p.terminal_mode == MGX_TERMINAL_TRUNCATED && r.trunc && !r.term));
-                s_rpt[lanev] = r.view;
-                o.reward[oi] = (float)r.rew;
-                if (o.reward64) o.reward64[oi] = r.rew;
-                o.term[oi] = r.term;
-                o.trunc[oi] = r.trunc;
-                o.done[oi] = r.done;
-                if (t == K - 1) {
-                    if (o.ep_ret) o.ep_ret[e] = (float)r.rew;    // only the final step can pay a reward
-                    if (o.ep_len) o.ep_len[e] = r.sc;
-                }
-                uint8_t mid = st.mission_id;
-                int lvl = 0;
-                if (r.done && (rpos_t)(s_pub[lanev] - rhead) != 0) {
-                    // SubprocVecEnv auto-reset: the staged ring episode (header, RNG snapshot, grid)
-                    popb = rhead & 1;
-                    const uint4 h = s_ph[popb * BLOCK_ENVS + lanev];
-                    if (p.has_move) s_mr[lanev] = p.ring_range[e * (uint32_t)D + (rhead & (D - 1))];
-                    mid = (uint8_t)(h.y >> 16);
-                    st.ax = (uint8_t)(h.x & 0xFF); st.ay = (uint8_t)((h.x >> 8) & 0xFF); st.dir = (uint8_t)((h.x >> 16) & 0xFF);
-                    st.carry = 0; st.step_count = 0; st.reward_step = (int16_t)r.rs;     // survives the reset (Q2)
-                    st.tx = (uint8_t)(h.x >> 24); st.ty = (uint8_t)h.y; st.target_action = (uint8_t)(h.y >> 8);
-                    st.mission_id = mid; st.mission_done = (uint8_t)r.mdone; st.frames = 1; st.flags = 0; st.pad = 0;
-                    s_rp[lanev] = h.x & 0xFFFFFFu;
-                    rhead++;
-                    s_head[lanev] = rhead;
-                    nh = rhead;
-                    atomicAdd(&s_cnt[0], 1ull);
-                    if (h.z) atomicAdd(&s_cnt[1], (unsigned long long)h.z);
-                    lvl = (int)h.z;
-                } else {
-                    if (r.done) err |= MGX_DEVERR_RING_EMPTY;   // cannot happen (refill production rule)
-                    st.ax = (uint8_t)(r.view & 0xFF); st.ay = (uint8_t)((r.view >> 8) & 0xFF);
-                    st.dir = (uint8_t)((r.view >> 16) & 3); st.carry = r.carry;
-                    st.step_count = (uint16_t)r.sc; st.reward_step = (int16_t)r.rs; st.mission_done = (uint8_t)r.mdone;
-                    s_rp[lanev] = r.view;
-                }
-                o.mids[oi] = mid;
-                if (t == K - 1 && o.livelock) o.livelock[e] = lvl;
-                {
-                    uint4 sv;
-                    __builtin_memcpy(&sv, &st, sizeof st);
-                    s_st[lanev] = sv;
-                }
-                if (err) atomicOr(&s_err, err);
-            }
-            s_term[lanev] = tw;
-            s_popb[lanev] = popb;
-            s_nh[tb][lanev] = nh;
-            const unsigned long long tm = __ballot(tw);
-            if (lanev == 0) s_tmask = tm;
-        }
-        RSTAMP(1);                                     // step logic (wave 0)
-        __syncthreads();
-        RSTAMP(2);                                     // wait for the block
-        // (every barrier below is reached by all five waves: the DMA wave's threads have le >= 64)
-        const int le = tidv >> 2, q = tidv & 3;
-        if (s_tmask) {
-            // terminal rows (rare, block-uniform): the finished episode's last view, rendered into the
-            // env's frame row from its post-step grid and copied out before the row is reused below
-            if (le < ne && s_term[le]) render_cols(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW + 1);
-            __syncthreads();
-            if (VIS) {
-                if (tidv < ne && s_term[tidv]) apply_vis(s_stk + tidv * FROW + 1);
+            __syncthreads();                                   // A
+            if (s_tmask) {
+                __syncthreads();
+                if (VIS) __syncthreads();
+                __syncthreads();
                 __syncthreads();
             }
-            if (tidv < ne && s_term[tidv]) s_stk[tidv * FROW] = (uint8_t)((s_rpt[tidv] >> 16) & 3);
-            __syncthreads();
-            if (le < ne && s_term[le]) {
-                const uint32_t *fr = reinterpret_cast<const uint32_t *>(s_stk + le * FROW);
-                uint32_t *tr = reinterpret_cast<uint32_t *>(o.t_rows + (e0 + le) * (int64_t)FROW);
-#pragma unroll 1
-                for (int k = 10 * q; k < min(10 * q + 10, FROW / 4); k++) tr[k] = fr[k];
+            if (VIS) {
+                __syncthreads();
+                __syncthreads();
             }
+            __builtin_amdgcn_s_waitcnt(0);                     // this step's prefetches have landed ...
+            __syncthreads();                                   // B: ... before the next step reads them
+        }
+    } else {
+        for (int t = 0; t < K; t++) {
+            const int tb = t & 1;
+            RSTAMP(0);
+            // thread index through an opaque copy: lane- / env-derived addresses are then computed inside
+            // each region of the step, instead of being hoisted out of the loop and kept live through all of
+            // them (96 -> fewer VGPRs; the render's and the step logic's registers no longer add up)
+            int tidv = tid;
+            asm volatile("" : "+v"(tidv));
+            const int lanev = tidv & (BLOCK_ENVS - 1);
+            if (wave0) {
+                // ---- the step: one lanev per env
+                bool tw = false;
+                uint8_t popb = 0xFF;
+                uint32_t nh = NO_POP;
+                if (lanev < ne) {
+                    const uint32_t e = (uint32_t)(e0 + lanev), oi = (uint32_t)t * (uint32_t)N + e;   // N * K < 2^32
+                    EnvState st;
+                    {
+                        const uint4 sv = s_st[lanev];
+                        __builtin_memcpy(&st, &sv, sizeof st);
+                    }
+                    rpos_t rhead = s_head[lanev];
+                    uint64_t mrange = MOVE ? s_mr[lanev] : 0ull;
+                    uint32_t err = 0;
+                    int a = s_act[tb * BLOCK_ENVS + lanev];
+                    if ((unsigned)a > 6u) { err |= MGX_DEVERR_BAD_ACTION; a = -1; }
+                    const StepRes r = env_step(st, a, s_grid, lanev, S, p.manual, mrange);
+                    tw = r.done && (p.terminal_mode == MGX_TERMINAL_ALL ||
+                                    (p.terminal_mode == MGX_TERMINAL_TRUNCATED && r.trunc && !r.term));
+                    s_rpt[lanev] = r.view;
+                    o.reward[oi] = (float)r.rew;
+                    if (R64) o.reward64[oi] = r.rew;
+                    o.term[oi] = r.term;
+                    o.trunc[oi] = r.trunc;
+                    o.done[oi] = r.done;
+                    if (t == K - 1) {                        // written out after the loop
+                        s_lrew[lanev] = (float)r.rew;        // (only the final step can pay a reward)
+                        s_lsc[lanev] = r.sc;
+                    }
+                    uint8_t mid = st.mission_id;
+                    int lvl = 0;
+                    if (r.done && (rpos_t)(s_pub[lanev] - rhead) != 0) {
+                        // SubprocVecEnv auto-reset: the staged ring episode (header, RNG snapshot, grid)
+                        popb = rhead & 1;
+                        const uint4 h = s_ph[popb * BLOCK_ENVS + lanev];
+                        if (MOVE) s_mr[lanev] = p.ring_range[e * (uint32_t)D + (rhead & (D - 1))];
+                        mid = (uint8_t)(h.y >> 16);
+                        st.ax = (uint8_t)(h.x & 0xFF); st.ay = (uint8_t)((h.x >> 8) & 0xFF); st.dir = (uint8_t)((h.x >> 16) & 0xFF);
+                        st.carry = 0; st.step_count = 0; st.reward_step = (int16_t)r.rs;     // survives the reset (Q2)
+                        st.tx = (uint8_t)(h.x >> 24); st.ty = (uint8_t)h.y; st.target_action = (uint8_t)(h.y >> 8);
+                        st.mission_id = mid; st.mission_done = (uint8_t)r.mdone; st.frames = 1; st.flags = 0; st.pad = 0;
+                        s_rp[lanev] = h.x & 0xFFFFFFu;
+                        rhead++;
+                        s_head[lanev] = rhead;
+                        nh = rhead;
+                        atomicAdd(&s_cnt[0], 1ull);
+                        if (h.z) atomicAdd(&s_cnt[1], (unsigned long long)h.z);
+                        lvl = (int)h.z;
+                    } else {
+                        if (r.done) err |= MGX_DEVERR_RING_EMPTY;   // cannot happen (refill production rule)
+                        st.ax = (uint8_t)(r.view & 0xFF); st.ay = (uint8_t)((r.view >> 8) & 0xFF);
+                        st.dir = (uint8_t)((r.view >> 16) & 3); st.carry = r.carry;
+                        st.step_count = (uint16_t)r.sc; st.reward_step = (int16_t)r.rs; st.mission_done = (uint8_t)r.mdone;
+                        s_rp[lanev] = r.view;
+                    }
+                    o.mids[oi] = mid;
+                    if (t == K - 1) s_lll[lanev] = lvl;
+                    {
+                        uint4 sv;
+                        __builtin_memcpy(&sv, &st, sizeof st);
+                        s_st[lanev] = sv;
+                    }
+                    if (err) atomicOr(&s_err, err);
+                }
+                s_term[lanev] = tw;
+                s_popb[lanev] = popb;
+                s_nh[tb][lanev] = nh;
+                const unsigned long long tm = __ballot(tw);
+                if (lanev == 0) s_tmask = tm;
+            }
+            RSTAMP(1);                                     // step logic (wave 0)
             __syncthreads();
+            RSTAMP(2);                                     // wait for the block
+            // (every barrier below is matched by the DMA wave's loop)
+            const int le = tidv >> 2, q = tidv & 3;
+            if (s_tmask) {
+                // terminal rows (rare, block-uniform): the finished episode's last view, rendered into the
+                // env's frame row from its post-step grid and copied out before the row is reused below
+                if (le < ne && s_term[le]) render_cols(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW + 1);
+                __syncthreads();
+                if (VIS) {
+                    if (tidv < ne && s_term[tidv]) apply_vis(s_stk + tidv * FROW + 1);
+                    __syncthreads();
+                }
+                if (tidv < ne && s_term[tidv]) s_stk[tidv * FROW] = (uint8_t)((s_rpt[tidv] >> 16) & 3);
+                __syncthreads();
+                if (le < ne && s_term[le]) {
+                    const uint32_t *fr = reinterpret_cast<const uint32_t *>(s_stk + le * FROW);
+                    uint32_t *tr = reinterpret_cast<uint32_t *>(o.t_rows + (e0 + le) * (int64_t)FROW);
+    #pragma unroll 1
+                    for (int k = 10 * q; k < min(10 * q + 10, FROW / 4); k++) tr[k] = fr[k];
+                }
+                __syncthreads();
+            }
+            // the frame of every env: the new episode's first where one was popped (rendered straight from
+            // its staged grid, which then becomes the env's grid)
+            if (le < ne) {
+                const uint8_t b = s_popb[le];
+                const uint8_t *g = b == 0xFF ? s_grid : s_pg + b * GB;
+                const uint32_t rp = s_rp[le];
+                render_cols(g, S, le, q, rp, s_stk + le * FROW + 1);
+                if (q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);
+                if (b != 0xFF)
+                    for (int c = q; c < GSQ; c += 4)
+                        *reinterpret_cast<uint4 *>(s_grid + c * (BLOCK_ENVS * 16) + le * 16) =
+                            *reinterpret_cast<const uint4 *>(g + c * (BLOCK_ENVS * 16) + le * 16);
+            }
+            if (VIS) {
+                __syncthreads();
+                if (tidv < ne) apply_vis(s_stk + tidv * FROW + 1);
+                __syncthreads();
+            }
+            RSTAMP(3);                                     // terminal rows + render
+            {
+                // rows out: per wave (its 16 rows, no barrier) or, after process_vis, per block
+                const bool wave_rows = !VIS;
+                const int r0 = wave_rows ? (tidv >> 6) * 16 : 0;
+                const int nr = wave_rows ? max(0, min(16, ne - r0)) : ne;
+                const int tt = wave_rows ? lanev : tidv, nt = wave_rows ? 64 : BLOCK_THREADS;
+                if (wave_rows) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                const int nb16 = (nr * FROW) >> 4;
+                const uint4 *src = reinterpret_cast<const uint4 *>(s_stk + r0 * FROW);
+                uint4 *dst = reinterpret_cast<uint4 *>(o.rows + ((int64_t)t * N + e0 + r0) * FROW);
+                for (int i = tt; i < nb16; i += nt) dst[i] = src[i];
+                const int rem = ((nr * FROW) >> 2) - (nb16 << 2);
+                if (tt < rem)
+                    reinterpret_cast<uint32_t *>(dst + nb16)[tt] = reinterpret_cast<const uint32_t *>(src + nb16)[tt];
+            }
+            __syncthreads();                               // B
+            RSTAMP(4);                                     // rows out + the block barrier
         }
-        // the frame of every env: the new episode's first where one was popped (rendered straight from
-        // its staged grid, which then becomes the env's grid)
-        if (le < ne) {
-            const uint8_t b = s_popb[le];
-            const uint8_t *g = b == 0xFF ? s_grid : s_pg + b * GB;
-            const uint32_t rp = s_rp[le];
-            render_cols(g, S, le, q, rp, s_stk + le * FROW + 1);
-            if (q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);
-            if (b != 0xFF)
-                for (int c = q; c < GSQ; c += 4)
-                    *reinterpret_cast<uint4 *>(s_grid + c * (BLOCK_ENVS * 16) + le * 16) =
-                        *reinterpret_cast<const uint4 *>(g + c * (BLOCK_ENVS * 16) + le * 16);
-        }
-        if (VIS) {
-            __syncthreads();
-            if (tidv < ne) apply_vis(s_stk + tidv * FROW + 1);
-            __syncthreads();
-        }
-        RSTAMP(3);                                     // terminal rows + render
-        if (!dmaw) {
-            // rows out: per wave (its 16 rows, no barrier) or, after process_vis, per block
-            const bool wave_rows = !VIS;
-            const int r0 = wave_rows ? (tidv >> 6) * 16 : 0;
-            const int nr = wave_rows ? max(0, min(16, ne - r0)) : ne;
-            const int tt = wave_rows ? lanev : tidv, nt = wave_rows ? 64 : BLOCK_THREADS;
-            if (wave_rows) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            const int nb16 = (nr * FROW) >> 4;
-            const uint4 *src = reinterpret_cast<const uint4 *>(s_stk + r0 * FROW);
-            uint4 *dst = reinterpret_cast<uint4 *>(o.rows + ((int64_t)t * N + e0 + r0) * FROW);
-            for (int i = tt; i < nb16; i += nt) dst[i] = src[i];
-            const int rem = ((nr * FROW) >> 2) - (nb16 << 2);
-            if (tt < rem)
-                reinterpret_cast<uint32_t *>(dst + nb16)[tt] = reinterpret_cast<const uint32_t *>(src + nb16)[tt];
-        }
-        // the DMA wave: this step's prefetches have landed before the next step reads them
-        if (dmaw) __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        RSTAMP(4);                                     // rows out + the block barrier
     }
 #if MGX_RSTAMPS
     if (tid == 0)
@@ -1455,7 +1485,10 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     if (wave0 && lane < ne) {
         reinterpret_cast<uint4 *>(p.state)[e0 + lane] = s_st[lane];
         p.ring_head[e0 + lane] = s_head[lane];
-        if (p.has_move) p.range_cur[e0 + lane] = s_mr[lane];
+        if (MOVE) p.range_cur[e0 + lane] = s_mr[lane];
+        if (o.ep_ret) o.ep_ret[e0 + lane] = s_lrew[lane];
+        if (o.ep_len) o.ep_len[e0 + lane] = s_lsc[lane];
+        if (o.livelock) o.livelock[e0 + lane] = s_lll[lane];
     }
     if (!dmaw) {
         uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * p.GS);
@@ -2621,8 +2654,13 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->lds_rollout = (size_t)((BLOCK_ENVS * FROW + 15) & ~15) + (size_t)BLOCK_ENVS * 3 * GS +
                      (size_t)BLOCK_ENVS * 2 * 16 + (size_t)2 * BLOCK_ENVS * 4 +
                      ((cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL) ? (size_t)BLOCK_ENVS * 8 : 0);
-    HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
-    HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
+#define MGX_ROLL_LDS(V, M, R)                                                                                     \
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<V, M, R>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                (int)h->lds_rollout))
+    MGX_ROLL_LDS(false, false, false); MGX_ROLL_LDS(false, false, true); MGX_ROLL_LDS(false, true, false);
+    MGX_ROLL_LDS(false, true, true); MGX_ROLL_LDS(true, false, false); MGX_ROLL_LDS(true, false, true);
+    MGX_ROLL_LDS(true, true, false); MGX_ROLL_LDS(true, true, true);
+#undef MGX_ROLL_LDS
     h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
     h->ext = cfg->obstacles || cfg->problem == MGX_PROBLEM_FULL || cfg->problem == MGX_PROBLEM_DRP ||
              cfg->problem == MGX_PROBLEM_MOV;
@@ -2946,12 +2984,21 @@ mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K,
         if (fs != MGX_OK) return fs;
     }
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
-    if (h->kp.vis)
-        hipLaunchKernelGGL(mgx_rollout_kernel<true>, dim3((unsigned)nblk), dim3(ROLL_THREADS), h->lds_rollout,
-                           (hipStream_t)stream, h->kp, o, actions_dev, K);
-    else
-        hipLaunchKernelGGL(mgx_rollout_kernel<false>, dim3((unsigned)nblk), dim3(ROLL_THREADS), h->lds_rollout,
-                           (hipStream_t)stream, h->kp, o, actions_dev, K);
+    const int var = (h->kp.vis ? 4 : 0) | (h->kp.has_move ? 2 : 0) | (o.reward64 ? 1 : 0);
+#define MGX_ROLL(V, M, R)                                                                                         \
+    hipLaunchKernelGGL((mgx_rollout_kernel<V, M, R>), dim3((unsigned)nblk), dim3(ROLL_THREADS), h->lds_rollout, \
+                       (hipStream_t)stream, h->kp, o, actions_dev, K)
+    switch (var) {
+        case 0: MGX_ROLL(false, false, false); break;
+        case 1: MGX_ROLL(false, false, true); break;
+        case 2: MGX_ROLL(false, true, false); break;
+        case 3: MGX_ROLL(false, true, true); break;
+        case 4: MGX_ROLL(true, false, false); break;
+        case 5: MGX_ROLL(true, false, true); break;
+        case 6: MGX_ROLL(true, true, false); break;
+        default: MGX_ROLL(true, true, true); break;
+    }
+#undef MGX_ROLL
     HIP_TRY(hipGetLastError());
     if (fork) {
         mgx_status fs = fork_end(h);

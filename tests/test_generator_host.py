@@ -47,7 +47,8 @@ def encode(codes, S):
 PROBLEMS = {"multi": 0, "full": 1, "gto": 2, "gtg": 3, "opn": 4, "pkp": 5, "drp": 6, "mov": 7}
 CASES = [("multi", 5, 8, 0, 0), ("multi", None, 8, 0, 0), ("multi", 1, 16, 0, 0), ("multi", 2, 11, 0, 0),
          ("multi", None, 8, 1, 0), ("multi", 0, 16, 1, 0), ("multi", None, 11, 0, 0), ("pkp", None, 8, 0, 0),
-         ("gtg", None, 8, 0, 0), ("multi", None, 8, 0, 4)]
+         ("gtg", None, 8, 0, 0), ("multi", None, 8, 0, 4), ("gtg", None, 8, 0, 1), ("mov", None, 8, 0, 2),
+         ("full", None, 11, 0, 0), ("pkp", None, 11, 0, 3), ("opn", None, 16, 0, 0)]
 
 
 @pytest.mark.parametrize("problem,mission,size,ado,nobst", CASES,
