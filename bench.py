@@ -225,7 +225,7 @@ def _allreduce(t, op):
     return t
 
 
-def main_ppo(args, world, rank, local, dev):
+def main_ppo(args, world, rank, local, dev, ranks_seen=1):
     """BASELINE config 3: PPO(CustomPPOPolicy) on PKP 8x8 with the engine (mgx/ppo.py)."""
     from mgx.policy import ActorCriticPolicy
     from mgx.ppo import PPOConfig, Trainer, make_collector
@@ -316,6 +316,7 @@ def main_ppo(args, world, rank, local, dev):
             "phases_s_per_iter": {"collect": tc / K, "train": tt / K},
             "eval": ev,
             "roofline": None,
+            "ranks_seen": ranks_seen, "dist_backend": dist.get_backend() if world > 1 else None,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -722,7 +723,7 @@ def main():
         ones = _allreduce(torch.ones(1, dtype=torch.float64, device=dev), dist.ReduceOp.SUM)
         ranks_seen = int(round(float(ones[0])))
     if args.workload == "ppo":
-        return main_ppo(args, world, rank, local, dev)
+        return main_ppo(args, world, rank, local, dev, ranks_seen)
     out = measure_rollout(args, args.layout, world, rank, dev)
     if world == 1 and args.both_layouts:
         # the other observation layouts on the same workload, reported beside the headline: one launch

@@ -1,9 +1,9 @@
 """Refill wave clocks (libmgx_rclock.so, -DMGX_REFILL_CLOCK): s_memtime cycles per wave per refill
-launch and attempt rounds per wave (the busiest lane's) -- run under rocprofv3 --kernel-trace with
-MGX_SERIAL_REFILL=1 to put the clocks beside the launch durations.
+launch and attempt rounds per wave (the busiest lane's) -- run under rocprofv3 --kernel-trace with a
+build that also has -DMGX_SERIAL_REFILL=1 to put the clocks beside the launch durations (mgx_diag.h).
 
 Env: MISSION (default 5), CAPS (space-separated production caps to sweep, default "0" = the engine's
-default), CAPMAX (space-separated MGX_REFILL_CAPMAX ceilings, default "0" = none), REFILL_EVERY (default 32).  One JSON line per cap: rounds per wave-launch against the
+default), REFILL_EVERY (default 32).  One JSON line per cap: rounds per wave-launch against the
 episodes each env consumed per launch (their ratio is the production overhead)."""
 import os, sys, json
 sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "minigrid-rl_amd")]
@@ -12,9 +12,7 @@ from mgx import MgxEngine
 n = 65536
 E = int(os.environ.get("REFILL_EVERY", 32))
 acts = torch.randint(0, 7, (2048, n), device="cuda", dtype=torch.int32)
-for cap, cmax in [(int(c), m) for c in os.environ.get("CAPS", "0").split()
-                  for m in os.environ.get("CAPMAX", "0").split()]:
-    os.environ["MGX_REFILL_CAPMAX"] = cmax
+for cap in [int(c) for c in os.environ.get("CAPS", "0").split()]:
     e = MgxEngine(problem="multi", mission=int(os.environ.get("MISSION", 5)), size=8, num_objects=4, n_envs=n,
                   terminal_mode="none", refill_every=E, refill_cap=cap)
     e.reset()
@@ -31,7 +29,7 @@ for cap, cmax in [(int(c), m) for c in os.environ.get("CAPS", "0").split()
     eps = (s1["resets"] - s0["resets"]) / n / launches
     rounds = (c1[27] - c0[27]) / waves
     hist = {r: c1[8 + r] - c0[8 + r] for r in range(16) if c1[8 + r] - c0[8 + r]}
-    print(json.dumps(dict(cap=cap, capmax=int(cmax), refill_every=E, rounds_hist=hist,
+    print(json.dumps(dict(cap=cap, refill_every=E, rounds_hist=hist,
                           slowest_wave_clocks=c1[29], queued_per_env=(s0["queued"] / n, s1["queued"] / n), launches=launches, clocks_per_wave_launch=(c1[26] - c0[26]) / waves,
                           rounds_per_wave_launch=rounds, episodes_per_env_launch=eps,
                           overhead=rounds / eps)), flush=True)

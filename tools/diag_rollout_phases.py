@@ -1,6 +1,6 @@
 """Fused-rollout phase clocks (libmgx_rstamps.so, -DMGX_RSTAMPS): s_memtime cycles per workgroup per
 step, wave 0's view -- step logic, wait at the post-logic barrier, terminal rows + render, rows out + the
-end-of-step barrier.  Env: N envs (65,536), MISSION (5), S (8); MGX_SERIAL_REFILL=1 runs the refill on the
+end-of-step barrier.  Env: N envs (65,536), MISSION (5), S (8); a -DMGX_SERIAL_REFILL=1 build (with -DMGX_RSTAMPS=1) runs the refill on the
 caller's stream (the rollout alone), else beside it."""
 import json
 import os
@@ -34,6 +34,6 @@ c1 = e.debug_counters()
 nblk = (n + 63) // 64
 steps = T // 2
 ph = [round((c1[k] - c0[k]) / nblk / steps) for k in range(4, 8)]
-print(json.dumps(dict(n=n, serial=os.environ.get("MGX_SERIAL_REFILL", "0"), us_per_step=round(dt / steps * 1e6, 2),
+print(json.dumps(dict(n=n, lib=os.path.basename(os.environ.get("MGX_LIB_PATH", "libmgx.so")), us_per_step=round(dt / steps * 1e6, 2),
                       clocks_per_block_step=dict(logic=ph[0], barrier_wait=ph[1], render=ph[2], rows_out_barrier=ph[3]),
                       total=sum(ph))))

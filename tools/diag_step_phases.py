@@ -1,6 +1,6 @@
 """Step-kernel phase clocks (libmgx_stamps.so, -DMGX_STAMPS=N): s_memtime cycles per workgroup per
 compact step, by phase (counters 4..7; their meaning depends on N, see mgx_step_kernel's tail).
-Env: N envs, MGX_SERIAL_REFILL=1 runs the refill on the caller's stream (step kernel alone)."""
+Env: N envs, a -DMGX_SERIAL_REFILL=1 build runs the refill on the caller's stream (step kernel alone)."""
 import os, sys, json, time
 sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'minigrid-rl_amd')]
 import torch
@@ -22,5 +22,5 @@ dt = time.perf_counter() - t0
 c1 = e.debug_counters()
 nblk = (n + 63) // 64
 ph = [round((c1[k] - c0[k]) / nblk / 128) for k in range(4, 8)]
-print(json.dumps(dict(n=n, serial=os.environ.get("MGX_SERIAL_REFILL", "0"), us_per_step=round(dt / 128 * 1e6, 2),
+print(json.dumps(dict(n=n, lib=os.path.basename(os.environ.get("MGX_LIB_PATH", "libmgx.so")), us_per_step=round(dt / 128 * 1e6, 2),
                       clocks_per_block_step=ph, total=sum(ph))))

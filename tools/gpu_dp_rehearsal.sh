@@ -15,3 +15,10 @@ for np in 2 4; do
 import json; d=json.load(open('$O/dp$np.line.json'))
 print('np $np n_gpus', d['n_gpus'], 'ranks_seen', d['ranks_seen'], 'backend', d['dist_backend'], 'value %.3e' % d['value'], d['config']['timed'])"
 done
+# the PPO workload (BASELINE config 3's loop) at 2 ranks: gradient + adv-stat all-reduces over gloo, each rank
+# its own 16,384-env shard
+MGX_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29510 bench.py --gpus 2 --workload ppo --n-envs 16384 --steps 2 --warmup 1 --eval-episodes 0 > $O/ppo2.json 2>$O/ppo2.err || { tail -20 $O/ppo2.err; exit 1; }
+grep '^{"metric"' $O/ppo2.json > $O/ppo2.line.json
+python -c "
+import json; d=json.load(open('$O/ppo2.line.json'))
+print('ppo np 2 n_gpus', d['n_gpus'], 'ranks_seen', d['ranks_seen'], d['dist_backend'], 'value %.3e' % d['value'], d['phases_s_per_iter'], d['config']['parallelism'])"

@@ -1,14 +1,15 @@
 #!/bin/bash
-# Refill cost by elimination (diagnostic builds libmgx_skip<k>.so, MGX_GEN_SKIP=k): refill alone per
-# epoch with generator sections skipped.
+# Refill cost by elimination: refill alone per epoch (serial refill) with generator sections skipped.
+# Builds (mgx_diag.h): libmgx_serial.so = EXTRA="-DMGX_SERIAL_REFILL=1", libmgx_skip<k>.so =
+# EXTRA="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=<k>" (make -C minigrid-rl_amd EXTRA=... OUT=mgx/<name>).
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-export MGX_SERIAL_REFILL=1
 for k in ${SKIPS:-"" 1 2 4 8}; do
-  L=$R/minigrid-rl_amd/mgx/libmgx${k:+_skip$k}.so
+  L=$R/minigrid-rl_amd/mgx/libmgx_serial.so
+  [ -n "$k" ] && L=$R/minigrid-rl_amd/mgx/libmgx_skip$k.so
   MGX_LIB_PATH=$L timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/skip$k -o run --output-format csv -- python3 $R/tools/refill_cost.py > $O/skip$k.log 2>&1 || { tail -20 $O/skip$k.log; exit 1; }
   python3 -c "
 import csv

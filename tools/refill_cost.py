@@ -1,4 +1,4 @@
-"""Refill-kernel cost per episode for a config (serial refill: run with MGX_SERIAL_REFILL=1 under
+"""Refill-kernel cost per episode for a config (serial refill: run a -DMGX_SERIAL_REFILL=1 build under
 rocprofv3 --kernel-trace --stats; the refill launches of the timed epochs are the kernel's calls minus
 the initial fill).  Prints resets consumed so the per-episode cost can be formed."""
 import os
