@@ -45,6 +45,15 @@
 #ifndef MGX_MT_WG1          // MT window groups per refill lane at S <= 8 (8 or 16; 16 for larger grids)
 #define MGX_MT_WG1 8
 #endif
+#ifndef MGX_ROLL_S8         // 1: S = 8 runs the rollout kernel compiled for S = 8 (0: the generic one)
+#define MGX_ROLL_S8 1
+#endif
+#ifndef MGX_REFILL_S8        // 1: S = 8 refills with the kernel compiled for S = 8 (0: the generic multi one)
+#define MGX_REFILL_S8 1
+#endif
+#ifndef MGX_ROLLOUT_FIRST    // 1: mgx_rollout_compact enqueues its rollout before the epoch's refill (0: after;
+#define MGX_ROLLOUT_FIRST 0  // round 4 A/B: rollout-first 4.0-4.2 vs 5.2-5.4 x 10^9 on the 20-step line)
+#endif
 #ifndef MGX_SERIAL_REFILL   // refill on the caller's stream (the refill alone, for timing it)
 #define MGX_SERIAL_REFILL 0
 #endif

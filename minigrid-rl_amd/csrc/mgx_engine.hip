@@ -1182,12 +1182,12 @@ constexpr int ROLL_THREADS = BLOCK_THREADS + 64;
 // step): VIS see_through_walls == False (Grid.process_vis), MOVE 'move' missions (problems mov / full: target
 // ranges), R64 the optional f64 rewards.  ep_return / ep_len / livelock (after the last step only) are kept in
 // LDS and written after the loop.
-template <bool VIS, bool MOVE, bool R64>
+template <bool VIS, bool MOVE, bool R64, int SC = 0>   // SC > 0: the grid size as a compile-time constant
 __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p, ROut o, const int32_t *__restrict__ actions,
                                                                       int K) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int CSTK = (BLOCK_ENVS * FROW + 15) & ~15;
-    const int GSQ = p.GS >> 4, GB = GSQ * BLOCK_ENVS * 16;
+    const int GSQ = SC > 0 ? ((SC * SC + 15) & ~15) >> 4 : p.GS >> 4, GB = GSQ * BLOCK_ENVS * 16;
     uint8_t *s_stk = smem;                                             // frame rows [64][148]
     uint8_t *s_grid = smem + CSTK;                                     // current grids (chunk-major, cm_off)
     uint8_t *s_pg = s_grid + GB;                                       // [2] staged ring episodes' grids
@@ -1217,7 +1217,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     const int64_t e0 = (int64_t)blockIdx.x * BLOCK_ENVS;
     const int64_t N = p.n;
     const int ne = (int)min<int64_t>(BLOCK_ENVS, N - e0);
-    const int S = p.S, D = p.D;
+    const int S = SC > 0 ? SC : p.S, D = p.D;
     const bool wave0 = tid < BLOCK_ENVS, dmaw = tid >= BLOCK_THREADS;
     const int lc = min(lane, ne - 1);
     // ---- setup: ring positions and state (waves 0 and 4), grids (waves 0-3, LDS-DMA)
@@ -1239,13 +1239,23 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + (h & (D - 1));   // N * D < 2^32
         const uint4 *hs = p.ring_hdr + 3 * slot;
         // the grid's byte offset is 64-bit: N * D * GS reaches 2^33 at config 5 (131,072 x 256 x 256)
-        const uint4 *gs = reinterpret_cast<const uint4 *>(p.ring_grid + (size_t)slot * (size_t)p.GS);
-        if (h & 1) {                                 // LDS-DMA destinations must be wave-uniform
-            __builtin_amdgcn_global_load_lds(hs, s_ph + BLOCK_ENVS, 16, 0, 0);
-            for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + GB + c * (BLOCK_ENVS * 16), 16, 0, 0);
-        } else {
+        const uint4 *gs = reinterpret_cast<const uint4 *>(p.ring_grid + (size_t)slot * (size_t)(GSQ << 4));
+        // LDS-DMA destinations (M0) must be wave-uniform: one pass per buffer, each under the exec mask of
+        // its lanes, as two separate branches -- NOT if / else.  From an if / else whose arms issue the same
+        // loads to different LDS bases, the compiler sank a common load (chunk 3 at S = 8, the loop unrolled)
+        // below the join and took its M0 from the first lane's arm (v_readfirstlane): the other parity's
+        // lanes wrote that chunk into the wrong buffer (round 4).  The asm barriers keep each pass's loads in
+        // its own branch.
+        const uint32_t par = h & 1;
+        if (par == 0) {
             __builtin_amdgcn_global_load_lds(hs, s_ph, 16, 0, 0);
             for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + c * (BLOCK_ENVS * 16), 16, 0, 0);
+            asm volatile("" ::: "memory");
+        }
+        if (par != 0) {
+            __builtin_amdgcn_global_load_lds(hs, s_ph + BLOCK_ENVS, 16, 0, 0);
+            for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + GB + c * (BLOCK_ENVS * 16), 16, 0, 0);
+            asm volatile("" ::: "memory");
         }
     };
     rpos_t head0 = 0;                                // the DMA wave: this env's ring head at the launch's start
@@ -1578,7 +1588,7 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
 // off the step kernel's critical path.  Episodes are generated in exactly the
 // order the env will consume them, so RNG streams advance as in the reference.
 // One wave per workgroup; all LDS is lane-private (grid row + MT window + objs).
-template <int NW, bool EXT, bool MULTI>
+template <int NW, bool EXT, bool MULTI, int SC = 0>   // SC > 0: the grid size as a compile-time constant
 __device__ __forceinline__ void refill_body(const KParams &p) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int tid = threadIdx.x;
@@ -1661,6 +1671,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         if (nfree > 0) {
             Gen<NW> G;
             load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
+            if (SC > 0) G.S = SC;                      // (p.S == SC: the host picks this kernel for it)
             load_rng(G, p, e);
             int livelocks = (int)(p.aux[e].y >> 1);   // abandoned attempts carried over from the last epoch
             // One attempt per iteration for every lane: a lane whose attempt live-locked retries
@@ -1755,6 +1766,9 @@ template <>
 __global__ __launch_bounds__(64, 3) void mgx_refill_multi_kernel<1>(KParams p) {
     refill_body<1, false, true>(p);
 }
+// ... at S = 8 (configs 2, 3 and 4): the grid size a constant -- room rectangles, the middle wall, the border
+// masks and every cell index fold into immediates (round 4)
+__global__ __launch_bounds__(64, 3) void mgx_refill_s8_kernel(KParams p) { refill_body<1, false, true, 8>(p); }
 
 // ============================================================== scene kernel
 // mgx_scene: regenerates env e's current episode from the RNG state its generation started from
@@ -2660,6 +2674,10 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     MGX_ROLL_LDS(false, false, false); MGX_ROLL_LDS(false, false, true); MGX_ROLL_LDS(false, true, false);
     MGX_ROLL_LDS(false, true, true); MGX_ROLL_LDS(true, false, false); MGX_ROLL_LDS(true, false, true);
     MGX_ROLL_LDS(true, true, false); MGX_ROLL_LDS(true, true, true);
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<false, false, false, 8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<false, false, true, 8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
 #undef MGX_ROLL_LDS
     h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
     h->ext = cfg->obstacles || cfg->problem == MGX_PROBLEM_FULL || cfg->problem == MGX_PROBLEM_DRP ||
@@ -2674,6 +2692,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     MGX_SET_LDS(mgx_refill_kernel, h->lds_refill);
     MGX_SET_LDS1(mgx_refill_multi_kernel<1>, h->lds_refill); MGX_SET_LDS1(mgx_refill_multi_kernel<2>, h->lds_refill);
     MGX_SET_LDS1(mgx_refill_multi_kernel<4>, h->lds_refill);
+    MGX_SET_LDS1(mgx_refill_s8_kernel, h->lds_refill);
     MGX_SET_LDS(mgx_fixup_kernel, h->lds_refill);
     MGX_SET_LDS(mgx_scene_kernel, h->lds_refill);
 #undef MGX_SET_LDS
@@ -2734,7 +2753,8 @@ static mgx_status launch_refill(mgx_handle *h, void *stream, hipEvent_t done = n
     const int64_t nblk = (h->kp.n + 63) / 64;
     if (h->refill_multi && !h->ext && h->kp.problem == MGX_PROBLEM_MULTI) {
         const dim3 g((unsigned)nblk), b(64);
-        if (h->nw == 1) hipLaunchKernelGGL((mgx_refill_multi_kernel<1>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
+        if (MGX_REFILL_S8 && h->nw == 1 && h->kp.S == 8) hipLaunchKernelGGL(mgx_refill_s8_kernel, g, b, h->lds_refill, (hipStream_t)stream, h->kp);
+        else if (h->nw == 1) hipLaunchKernelGGL((mgx_refill_multi_kernel<1>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
         else if (h->nw == 2) hipLaunchKernelGGL((mgx_refill_multi_kernel<2>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
         else hipLaunchKernelGGL((mgx_refill_multi_kernel<4>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
     } else {
@@ -2974,23 +2994,24 @@ mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K,
     o.ep_ret = out->ep_return_dev;
     o.ep_len = out->ep_len_dev;
     o.livelock = out->livelock_dev;
-    // The rollout is launched BEFORE the epoch's refill is (both start from the same fork point): its
-    // workgroups take their CU slots first and the refill's waves fill the rest, in eager streams and in a
-    // captured hipGraph alike.  (With the refill enqueued first, a graph replay dispatched the refill's 1,024
-    // waves first and the 20-step rollout took 181 instead of 133 us: tools/trace_epochs.py, round 4.)
+    // Launch order of the epoch's refill and this rollout (both start from the same fork point):
+    // MGX_ROLLOUT_FIRST.  Refill first is the default: with the rollout first, its workgroups took the CU
+    // slots and the refill's waves, the longer of the two, started late (20-step line 4.0-4.2 vs
+    // 5.2-5.4 x 10^9 env-steps/s, tools/gpu_r4_refill_ab.sh), although the rollout alone is shorter then.
     const bool fork = h->calls % E == 0;
     if (fork) {
-        mgx_status fs = fork_begin(h, stream);
+        mgx_status fs = MGX_ROLLOUT_FIRST ? fork_begin(h, stream) : fork_refill(h, stream);
         if (fs != MGX_OK) return fs;
     }
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
     const int var = (h->kp.vis ? 4 : 0) | (h->kp.has_move ? 2 : 0) | (o.reward64 ? 1 : 0);
-#define MGX_ROLL(V, M, R)                                                                                         \
-    hipLaunchKernelGGL((mgx_rollout_kernel<V, M, R>), dim3((unsigned)nblk), dim3(ROLL_THREADS), h->lds_rollout, \
-                       (hipStream_t)stream, h->kp, o, actions_dev, K)
+#define MGX_ROLL(V, M, R, ...)                                                                                    \
+    hipLaunchKernelGGL((mgx_rollout_kernel<V, M, R, ##__VA_ARGS__>), dim3((unsigned)nblk), dim3(ROLL_THREADS),   \
+                       h->lds_rollout, (hipStream_t)stream, h->kp, o, actions_dev, K)
     switch (var) {
-        case 0: MGX_ROLL(false, false, false); break;
-        case 1: MGX_ROLL(false, false, true); break;
+        // S = 8 (configs 2, 3 and 4): the grid size a constant (render and grid-copy address math in immediates)
+        case 0: if (MGX_ROLL_S8 && h->kp.S == 8) MGX_ROLL(false, false, false, 8); else MGX_ROLL(false, false, false, 0); break;
+        case 1: if (MGX_ROLL_S8 && h->kp.S == 8) MGX_ROLL(false, false, true, 8); else MGX_ROLL(false, false, true, 0); break;
         case 2: MGX_ROLL(false, true, false); break;
         case 3: MGX_ROLL(false, true, true); break;
         case 4: MGX_ROLL(true, false, false); break;
@@ -3000,7 +3021,7 @@ mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K,
     }
 #undef MGX_ROLL
     HIP_TRY(hipGetLastError());
-    if (fork) {
+    if (fork && MGX_ROLLOUT_FIRST) {
         mgx_status fs = fork_end(h);
         if (fs != MGX_OK) return fs;
     }

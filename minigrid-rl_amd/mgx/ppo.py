@@ -364,18 +364,26 @@ def make_collector(engine, policy, cfg):
     raise ValueError("layout must be 'compact' or 'sb3'")
 
 
-def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None, callback=None, evaluate=False):
+def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None, callback=None, evaluate=False,
+          init=None):
     """PPO(...).learn(total_timesteps, callback=callback) for one rank's env shard; returns
     (policy, history, engine).  evaluate=True then runs evaluate_policy(model, vec_env,
     n_eval_episodes) on the training engine as src/ppo.py:161-165 does (history[-1]
-    gets mean_reward / std_reward)."""
+    gets mean_reward / std_reward).  init: continue a run (SB3's PPO.load(...) then
+    learn(..., reset_num_timesteps=False)): {"policy": state_dict, "optimizer": state_dict,
+    "timesteps": int, "seed_offset": int} -- the envs restart from fresh episodes seeded
+    cfg.seed + seed_offset; the learning-rate schedule continues from `timesteps`."""
     from .policy import ActorCriticPolicy
-    torch.manual_seed(cfg.seed + rank)
-    eng = MgxEngine(n_envs=cfg.n_envs, seed=cfg.seed, env_index_offset=rank * cfg.n_envs,
+    init = init or {}
+    torch.manual_seed(cfg.seed + rank + init.get("seed_offset", 0))
+    eng = MgxEngine(n_envs=cfg.n_envs, seed=cfg.seed + init.get("seed_offset", 0), env_index_offset=rank * cfg.n_envs,
                     n_stack=cfg.n_frames_stack, terminal_mode="truncated", mission_dtype=torch.uint8,
                     device=device, reward64=True, **cfg.env)
     pol = ActorCriticPolicy(n_stack=cfg.n_frames_stack, optim_eps=cfg.optim_eps, lr=cfg.initial_learning_rate,
                             mission_cache=cfg.mission_cache).to(eng.device)
+    if "policy" in init:
+        pol.load_state_dict(init["policy"])
+        pol.optimizer.load_state_dict(init["optimizer"])
     if group is not None:   # identical initial weights on every rank
         for p in pol.parameters():
             torch.distributed.broadcast(p.data, 0, group=group)
@@ -384,6 +392,7 @@ def learn(cfg, total_timesteps, device="cuda", group=None, rank=0, log=None, cal
     col.start()
     hist = []
     world = tr.world
+    col.num_timesteps = int(init.get("timesteps", 0)) // world
     while col.num_timesteps * world < total_timesteps:
         buf = col.collect(callback)
         if buf is None:                # callback asked to stop (SB3: continue_training False)

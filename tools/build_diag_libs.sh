@@ -1,0 +1,35 @@
+#!/bin/bash
+# Builds the diagnostic variants of libmgx.so (switches: csrc/mgx_diag.h) from the current sources, in
+# parallel, next to the product library (minigrid-rl_amd/mgx/libmgx_<name>.so; git-ignored, shipped to the GPU
+# box with the tree).  Usage: bash tools/build_diag_libs.sh [name ...]  (default: all below).
+set -e
+cd "$(dirname "$0")/../minigrid-rl_amd"
+declare -A V=(
+  [serial]="-DMGX_SERIAL_REFILL=1"
+  [rstamps]="-DMGX_RSTAMPS=1"
+  [rstamps_serial]="-DMGX_RSTAMPS=1 -DMGX_SERIAL_REFILL=1"
+  [rclock]="-DMGX_REFILL_CLOCK=1"
+  [nos8]="-DMGX_ROLL_S8=0"
+  [skip1]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=1"
+  [skip2]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=2"
+  [skip4]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=4"
+  [skip8]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=8"
+  [skip32]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=32"
+  [nos8r]="-DMGX_REFILL_S8=0"
+  [rollfirst]="-DMGX_ROLLOUT_FIRST=1"
+  [bres]="-DMGX_REFILL_ROUNDS=2"
+  [nos8r_serial]="-DMGX_REFILL_S8=0 -DMGX_SERIAL_REFILL=1"
+  [wg16_serial]="-DMGX_MT_WG1=16 -DMGX_SERIAL_REFILL=1"
+)
+names=("$@")
+[ ${#names[@]} -eq 0 ] && names=("${!V[@]}")
+pids=()
+for n in "${names[@]}"; do
+  make -s -B EXTRA="${V[$n]}" OUT=mgx/libmgx_$n.so > /tmp/build_diag_$n.log 2>&1 &
+  pids+=($!)
+  while [ $(jobs -rp | wc -l) -ge 4 ]; do sleep 1; done
+done
+rc=0
+for p in "${pids[@]}"; do wait $p || rc=1; done
+[ $rc -eq 0 ] || { echo "a diag build failed: /tmp/build_diag_*.log"; exit 1; }
+echo "built: ${names[*]}"

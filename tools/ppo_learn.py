@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--max-seconds", type=float, default=0, help="stop training after this long (then evaluate)")
     ap.add_argument("--progress", default=None, help="append one JSON line per rollout here")
+    ap.add_argument("--save", default=None, help="checkpoint (policy, optimizer, timesteps, curve) written here")
+    ap.add_argument("--resume", default=None, help="continue the run saved here (--timesteps stays the total)")
+    ap.add_argument("--no-eval", action="store_true", help="skip the evaluation (an intermediate segment)")
     args = ap.parse_args()
     from mgx.ppo import PPOConfig, learn
     mission = None if args.mission == "None" else int(args.mission)
@@ -63,7 +66,13 @@ def main():
     cfg = PPOConfig(n_envs=args.n_envs, horizon=args.horizon, batch_size=args.batch_size, n_epochs=args.epochs,
                     initial_learning_rate=args.lr0, final_learning_rate=args.lr1, env=env_kw)
     t0 = time.perf_counter()
-    curve = []
+    curve, init, prior_s, segment = [], None, 0.0, 0
+    if args.resume:                                    # our own checkpoint: tensors, ints and lists only
+        ck = torch.load(args.resume, map_location="cuda", weights_only=True)
+        curve, prior_s, segment = ck["curve"], float(ck["train_seconds"]), int(ck["segment"]) + 1
+        init = {"policy": ck["policy"], "optimizer": ck["optimizer"], "timesteps": int(ck["timesteps"]),
+                "seed_offset": 1000003 * segment}
+        t0 -= prior_s
 
     class Stop:                                        # SB3-style callback: False ends learn()
         def on_step(self, policy, num_timesteps):
@@ -78,10 +87,19 @@ def main():
                     f.write(json.dumps(curve[-1]) + "\n")
             if len(curve) % 10 == 1:
                 print("t=%.0fs %s" % (time.perf_counter() - t0, json.dumps(curve[-1])), file=sys.stderr, flush=True)
-    random_eval = success_rate(None, env_kw, args.eval_episodes, seed=4242)
-    pol, hist, eng = learn(cfg, int(args.timesteps), log=log, callback=Stop())
-    train_s = time.perf_counter() - t0
+    random_eval = None if args.no_eval else success_rate(None, env_kw, args.eval_episodes, seed=4242)
+    t_start = time.perf_counter()
+    pol, hist, eng = learn(cfg, int(args.timesteps), log=log, callback=Stop(), init=init)
+    train_s = prior_s + time.perf_counter() - t_start
     eng.close()
+    steps_done = hist[-1]["timesteps"] if hist else (init or {}).get("timesteps", 0)
+    if args.save:
+        torch.save({"policy": pol.state_dict(), "optimizer": pol.optimizer.state_dict(), "timesteps": steps_done,
+                    "curve": curve, "train_seconds": train_s, "segment": segment}, args.save)
+    if args.no_eval:
+        print(json.dumps({"segment": segment, "timesteps": steps_done, "train_seconds": train_s,
+                          "last": curve[-1] if curve else None}))
+        return
     ev = success_rate(pol, env_kw, args.eval_episodes, seed=4242)
     names = {2: "PKP", 5: "GTG", 0: "GTO", 1: "TGL", None: "ALL"}
     # README.md:54-65's table: the model evaluated on every task (columns GTG GTO PKP TGL ALL)
@@ -95,8 +113,8 @@ def main():
                       cfg.horizon // cfg.batch_size, "lr": [cfg.initial_learning_rate, cfg.final_learning_rate],
                       "other_hyperparameters": "algorithm/ppo.yaml (gamma, gae_lambda, clip ranges, ent/vf coef, "
                                                "max_grad_norm)"},
-           "timesteps": hist[-1]["timesteps"] if hist else 0, "rollouts": len(hist), "train_seconds": train_s,
-           "env_steps_per_s_incl_training": (hist[-1]["timesteps"] / train_s) if hist else None,
+           "timesteps": steps_done, "rollouts": len(curve), "segments": segment + 1, "train_seconds": train_s,
+           "env_steps_per_s_incl_training": steps_done / train_s if train_s else None,
            "eval": ev, "eval_random_policy": random_eval,
            "reference": ("README.md:65 PPO ALL model: GTG 75%, GTO 65%, PKP 59%, TGL 58%, ALL 65% (1k episodes; trained "
                          "through the all0..all6 curriculum, README.md:40-46; size and training steps unstated)"

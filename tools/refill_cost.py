@@ -12,7 +12,7 @@ from mgx import MgxEngine  # noqa: E402
 nobj = int(os.environ.get("NOBJ", 4))
 mission = os.environ.get("MISSION", "5")
 mission = None if mission == "None" else int(mission)
-n = 65536
+n = int(os.environ.get("N", 65536))
 e = MgxEngine(problem=os.environ.get("PROBLEM", "multi"), mission=mission, size=int(os.environ.get("S", 8)),
               num_objects=nobj, n_envs=n, terminal_mode="none", refill_every=32,
               all_doors_open=os.environ.get("ADO", "0") == "1")
@@ -22,4 +22,4 @@ for i in range(1024):
     e.step(acts[i])
 torch.cuda.synchronize()
 st = e.stats()
-print("nobj", nobj, "mission", mission, "resets", st["resets"], "refill_launches", st["refill_launches"])
+print("nobj", nobj, "mission", mission, "resets", st["resets"], "refill_launches", st["refill_launches"], "n", n)
