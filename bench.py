@@ -549,7 +549,11 @@ def measure_rollout(args, layout, world, rank, dev):
     windows, cur = [], None
     if fused:
         # one window per launch (one refill epoch of E steps); the previous epoch's refill is joined
-        # before the window opens, so the window holds the epoch's fork (ring_pub copy) and the kernel
+        # before the window opens, so the window holds the epoch's fork and the kernel.  A spin kernel
+        # first keeps the GPU busy while the host enqueues every window (round 4: without it each window
+        # also held the host's time to enqueue the refill ahead of the rollout, ~19 us per launch)
+        if hasattr(torch.cuda, "_sleep"):
+            torch.cuda._sleep(int((P // E) * 60e-6 * 2.4e9))
         for t in range(0, P - P % E, E):
             eng.join()
             w = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), E]

@@ -8,16 +8,16 @@ declare -A V=(
   [serial]="-DMGX_SERIAL_REFILL=1"
   [rstamps]="-DMGX_RSTAMPS=1"
   [rstamps_serial]="-DMGX_RSTAMPS=1 -DMGX_SERIAL_REFILL=1"
-  [rclock]="-DMGX_REFILL_CLOCK=1"
+  [rclock]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1"
   [nos8]="-DMGX_ROLL_S8=0"
-  [skip1]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=1"
-  [skip2]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=2"
-  [skip4]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=4"
-  [skip8]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=8"
-  [skip32]="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=32"
+  [skip1]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=1"
+  [skip2]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=2"
+  [skip4]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=4"
+  [skip8]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=8"
+  [skip32]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=32"
   [nos8r]="-DMGX_REFILL_S8=0"
   [rollfirst]="-DMGX_ROLLOUT_FIRST=1"
-  [bres]="-DMGX_REFILL_ROUNDS=2"
+  [r3rounds]="-DMGX_REFILL_ROUNDS=1"
   [nos8r_serial]="-DMGX_REFILL_S8=0 -DMGX_SERIAL_REFILL=1"
   [wg16_serial]="-DMGX_MT_WG1=16 -DMGX_SERIAL_REFILL=1"
 )

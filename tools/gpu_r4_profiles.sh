@@ -16,8 +16,12 @@ for shape in ${SHAPES:-2:fused:20 2:fused:2048 2:compact:20 4:fused:2048 5:fused
   if [ $steps -eq 20 ]; then E=20; else E=64; fi
   tag=${cfg}_${lay}_e$E
   B="$R/bench.py --config $cfg --layout $lay --both-layouts 0 --cpu-seconds 0 --steps $steps --warmup 5"
+  # the driver's own command, unchanged, for its line (config 2, fused, 20 steps: what BENCH_r04 times)
+  [ "$shape" = "2:fused:20" ] && B="$R/bench.py --gpus 1 --steps 20 --warmup 5"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/s_$tag -o run --output-format csv -- python3 $B > $O/s_$tag.log 2>&1 || { tail -20 $O/s_$tag.log; exit 1; }
   cp $(find $O/s_$tag -name '*kernel_stats.csv' | head -1) $O/kernel_stats_$tag.csv
+  gzip -c $(find $O/s_$tag -name '*kernel_trace.csv' | head -1) > $O/kernel_trace_$tag.csv.gz
+  grep '^{"metric"' $O/s_$tag.log > $O/bench_$tag.json || true
   timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $O/f_$tag -o run -- python3 $B > $O/f_$tag.log 2>&1 || { tail -20 $O/f_$tag.log; exit 1; }
   timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $O/w_$tag -o run -- python3 $B > $O/w_$tag.log 2>&1 || { tail -20 $O/w_$tag.log; exit 1; }
   if [ $lay = fused ]; then K=mgx_rollout_kernel; SPL=$E; else K="mgx_step_kernel<int, true>"; SPL=1; fi

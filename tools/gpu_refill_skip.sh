@@ -1,7 +1,7 @@
 #!/bin/bash
 # Refill cost by elimination: refill alone per epoch (serial refill) with generator sections skipped.
 # Builds (mgx_diag.h): libmgx_serial.so = EXTRA="-DMGX_SERIAL_REFILL=1", libmgx_skip<k>.so =
-# EXTRA="-DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=<k>" (make -C minigrid-rl_amd EXTRA=... OUT=mgx/<name>).
+# EXTRA="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=<k>" (tools/build_diag_libs.sh).
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out
