@@ -70,5 +70,5 @@
 #define MGX_REFILL_MEAN 2   // wave's mean consumption since its previous refill, rounded up
 #endif
 #ifndef MGX_REFILL_ROUNDS   // grid-wide ceiling of a wave's attempt rounds per epoch: 2 the Bresenham round cap
-#define MGX_REFILL_ROUNDS 1 // of mgx_mt_slide_kernel (round 4), 1 the grid's mean consumption + 1/4 rounded up
+#define MGX_REFILL_ROUNDS 2 // of mgx_mt_slide_kernel (round 4), 1 the grid's mean consumption + 1/4 rounded up
 #endif                      // (round 3), 0 none
