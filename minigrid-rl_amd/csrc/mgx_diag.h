@@ -51,6 +51,9 @@
 #ifndef MGX_REFILL_S8        // 1: S = 8 refills with the kernel compiled for S = 8 (0: the generic multi one)
 #define MGX_REFILL_S8 1
 #endif
+#ifndef MGX_REFILL_EPW       // envs per S = 8 refill wave: 0 auto (32 when 64-env waves leave SIMDs idle), 32, 64
+#define MGX_REFILL_EPW 0
+#endif
 #ifndef MGX_ROLLOUT_FIRST    // 1: mgx_rollout_compact enqueues its rollout before the epoch's refill (0: after;
 #define MGX_ROLLOUT_FIRST 0  // round 4 A/B: rollout-first 4.0-4.2 vs 5.2-5.4 x 10^9 on the 20-step line)
 #endif

@@ -130,8 +130,9 @@ struct KParams {
     uint32_t *fix_list;     // [N] envs whose ring was empty at their reset (mgx_fixup_kernel)
     uint32_t *fix_count;    // list length; fix_done: workgroups of the fixup kernel that finished
     uint32_t *fix_done;
-    ulonglong4 *blk;        // [3 * nblk] per-workgroup stats: step/reset | fixup | refill workgroups
+    ulonglong4 *blk;        // [4 * nblk] per-workgroup stats: step/reset | fixup | refill waves (x2)
     int nblk;               // ceil(N / 64)
+    int refill_epw;         // envs per refill wave at S = 8: 64, or 32 when 64-env waves leave SIMDs idle
     int D;
     int K;                  // refill epoch (steps)
     int cap;                // episodes an env produces per epoch beyond what the invariant needs (<0: fill to D)
@@ -1588,11 +1589,13 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
 // off the step kernel's critical path.  Episodes are generated in exactly the
 // order the env will consume them, so RNG streams advance as in the reference.
 // One wave per workgroup; all LDS is lane-private (grid row + MT window + objs).
-template <int NW, bool EXT, bool MULTI, int SC = 0>   // SC > 0: the grid size as a compile-time constant
+// EPW: envs per wave (64, or 32 with lanes 32-63 idle: twice the waves, each running the union of fewer
+// lanes' paths -- for grids whose 64-env waves would leave SIMDs without a refill wave, config 4).
+template <int NW, bool EXT, bool MULTI, int SC = 0, int EPW = 64>   // SC > 0: the grid size as a constant
 __device__ __forceinline__ void refill_body(const KParams &p) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int tid = threadIdx.x;
-    const int64_t e = (int64_t)blockIdx.x * 64 + tid;
+    const int64_t e = tid < EPW ? (int64_t)blockIdx.x * EPW + tid : INT64_MAX;   // idle lanes: e >= n
     uint8_t *s_grid = smem;                                   // [64][GSL]
     uint8_t *s_scr = smem + ((64 * p.GSL + 15) & ~15);        // [64] windows + objs
     unsigned long long maxcur = 0;
@@ -1743,7 +1746,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     int csum = e < p.n ? cons : 0;
     for (int off = 32; off > 0; off >>= 1) csum += __shfl_xor(csum, off);
     if (tid == 0) {
-        ulonglong4 b = p.blk[2 * p.nblk + blockIdx.x];
+        ulonglong4 b = p.blk[2 * p.nblk + blockIdx.x];   // (32-env waves: two slots per 64 envs)
         b.w = b.w > maxcur ? b.w : maxcur;
         b.x = (unsigned long long)csum;
         p.blk[2 * p.nblk + blockIdx.x] = b;
@@ -1768,7 +1771,8 @@ __global__ __launch_bounds__(64, 3) void mgx_refill_multi_kernel<1>(KParams p) {
 }
 // ... at S = 8 (configs 2, 3 and 4): the grid size a constant -- room rectangles, the middle wall, the border
 // masks and every cell index fold into immediates (round 4)
-__global__ __launch_bounds__(64, 3) void mgx_refill_s8_kernel(KParams p) { refill_body<1, false, true, 8>(p); }
+template <int EPW>
+__global__ __launch_bounds__(64, 3) void mgx_refill_s8_kernel(KParams p) { refill_body<1, false, true, 8, EPW>(p); }
 
 // ============================================================== scene kernel
 // mgx_scene: regenerates env e's current episode from the RNG state its generation started from
@@ -1876,7 +1880,9 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     unsigned long long cs = 0;
     if (tid < SLIDE_ENVS / 64) {
         const int64_t b = e0 / 64 + tid;
-        if (b < p.nblk) cs = p.blk[2 * p.nblk + b].x;
+        if (b < p.nblk)
+            cs = p.refill_epw == 32 ? p.blk[2 * p.nblk + 2 * b].x + p.blk[2 * p.nblk + 2 * b + 1].x
+                                    : p.blk[2 * p.nblk + b].x;
     }
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long o = __shfl_xor(mn, off), q = __shfl_xor(mx, off);
@@ -2623,9 +2629,18 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.fix_done = p.fix_list + N + 8;
     p.nblk = (int)((N + 63) / 64);
     {
-        hipError_t e = hipMalloc(&h->allocs[13], (size_t)3 * p.nblk * sizeof(ulonglong4));
+        // 32-env refill waves when 64-env ones would not give every SIMD one (config 4: 512 waves for
+        // 1,024 SIMDs); MGX_REFILL_EPW forces 32 or 64
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+        p.refill_epw = MGX_REFILL_EPW == 32 || MGX_REFILL_EPW == 64 ? MGX_REFILL_EPW : (p.nblk < 4 * cus ? 32 : 64);
+    }
+    {
+        // sections: [0, nblk) steps, [nblk, 2 nblk) fixup, [2 nblk, 4 nblk) refill waves (two per 64 envs
+        // with 32-env waves)
+        hipError_t e = hipMalloc(&h->allocs[13], (size_t)4 * p.nblk * sizeof(ulonglong4));
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc stats"));
-        e = hipMemset(h->allocs[13], 0, (size_t)3 * p.nblk * sizeof(ulonglong4));
+        e = hipMemset(h->allocs[13], 0, (size_t)4 * p.nblk * sizeof(ulonglong4));
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset stats"));
         p.blk = (ulonglong4 *)h->allocs[13];
     }
@@ -2692,7 +2707,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     MGX_SET_LDS(mgx_refill_kernel, h->lds_refill);
     MGX_SET_LDS1(mgx_refill_multi_kernel<1>, h->lds_refill); MGX_SET_LDS1(mgx_refill_multi_kernel<2>, h->lds_refill);
     MGX_SET_LDS1(mgx_refill_multi_kernel<4>, h->lds_refill);
-    MGX_SET_LDS1(mgx_refill_s8_kernel, h->lds_refill);
+    MGX_SET_LDS1(mgx_refill_s8_kernel<64>, h->lds_refill);
+    MGX_SET_LDS1(mgx_refill_s8_kernel<32>, h->lds_refill);
     MGX_SET_LDS(mgx_fixup_kernel, h->lds_refill);
     MGX_SET_LDS(mgx_scene_kernel, h->lds_refill);
 #undef MGX_SET_LDS
@@ -2753,7 +2769,13 @@ static mgx_status launch_refill(mgx_handle *h, void *stream, hipEvent_t done = n
     const int64_t nblk = (h->kp.n + 63) / 64;
     if (h->refill_multi && !h->ext && h->kp.problem == MGX_PROBLEM_MULTI) {
         const dim3 g((unsigned)nblk), b(64);
-        if (MGX_REFILL_S8 && h->nw == 1 && h->kp.S == 8) hipLaunchKernelGGL(mgx_refill_s8_kernel, g, b, h->lds_refill, (hipStream_t)stream, h->kp);
+        if (MGX_REFILL_S8 && h->nw == 1 && h->kp.S == 8) {
+            if (h->kp.refill_epw == 32)
+                hipLaunchKernelGGL(mgx_refill_s8_kernel<32>, dim3((unsigned)((h->kp.n + 31) / 32)), b, h->lds_refill,
+                                   (hipStream_t)stream, h->kp);
+            else
+                hipLaunchKernelGGL(mgx_refill_s8_kernel<64>, g, b, h->lds_refill, (hipStream_t)stream, h->kp);
+        }
         else if (h->nw == 1) hipLaunchKernelGGL((mgx_refill_multi_kernel<1>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
         else if (h->nw == 2) hipLaunchKernelGGL((mgx_refill_multi_kernel<2>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
         else hipLaunchKernelGGL((mgx_refill_multi_kernel<4>), g, b, h->lds_refill, (hipStream_t)stream, h->kp);
@@ -3149,10 +3171,10 @@ mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]) {
     if (!h || !out) return fail(MGX_ERR_INVALID, "null argument");
     HIP_TRY(hipStreamSynchronize(h->side));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    std::vector<ulonglong4> b((size_t)3 * h->kp.nblk);
+    std::vector<ulonglong4> b((size_t)4 * h->kp.nblk);
     HIP_TRY(hipMemcpy(b.data(), h->kp.blk, b.size() * sizeof(ulonglong4), hipMemcpyDeviceToHost));
     uint64_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // blk sections: [0, nblk) step kernel (x steps, y resets), [nblk, 2 nblk) fixup, [2 nblk, 3 nblk)
+    // blk sections: [0, nblk) step kernel (x steps, y resets), [nblk, 2 nblk) fixup, [2 nblk, 4 nblk)
     // refill (x: that wave's consumption at its last launch, not a counter); z live-locks and w max MT cursor
     // in every section
     for (size_t i = 0; i < b.size(); i++) {

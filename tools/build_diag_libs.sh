@@ -17,6 +17,8 @@ declare -A V=(
   [skip32]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=32"
   [nos8r]="-DMGX_REFILL_S8=0"
   [rollfirst]="-DMGX_ROLLOUT_FIRST=1"
+  [epw64]="-DMGX_REFILL_EPW=64"
+  [epw32]="-DMGX_REFILL_EPW=32"
   [r3rounds]="-DMGX_REFILL_ROUNDS=1"
   [nos8r_serial]="-DMGX_REFILL_S8=0 -DMGX_SERIAL_REFILL=1"
   [wg16_serial]="-DMGX_MT_WG1=16 -DMGX_SERIAL_REFILL=1"
