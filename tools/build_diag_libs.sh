@@ -19,6 +19,9 @@ declare -A V=(
   [rollfirst]="-DMGX_ROLLOUT_FIRST=1"
   [epw64]="-DMGX_REFILL_EPW=64"
   [epw32]="-DMGX_REFILL_EPW=32"
+  [prio3]="-DMGX_REFILL_PRIO=3"
+  [topup4]="-DMGX_MT_TOPUP=4"
+  [topup2]="-DMGX_MT_TOPUP=2"
   [r3rounds]="-DMGX_REFILL_ROUNDS=1"
   [nos8r_serial]="-DMGX_REFILL_S8=0 -DMGX_SERIAL_REFILL=1"
   [wg16_serial]="-DMGX_MT_WG1=16 -DMGX_SERIAL_REFILL=1"
