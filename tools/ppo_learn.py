@@ -65,7 +65,7 @@ def main():
     env_kw = dict(problem="multi", mission=mission, size=args.size, num_objects=4)
     cfg = PPOConfig(n_envs=args.n_envs, horizon=args.horizon, batch_size=args.batch_size, n_epochs=args.epochs,
                     initial_learning_rate=args.lr0, final_learning_rate=args.lr1, env=env_kw)
-    t0 = time.perf_counter()
+    t0 = t_seg = time.perf_counter()
     curve, init, prior_s, segment = [], None, 0.0, 0
     if args.resume:                                    # our own checkpoint: tensors, ints and lists only
         ck = torch.load(args.resume, map_location="cuda", weights_only=True)
@@ -76,7 +76,8 @@ def main():
 
     class Stop:                                        # SB3-style callback: False ends learn()
         def on_step(self, policy, num_timesteps):
-            return not (args.max_seconds and time.perf_counter() - t0 > args.max_seconds)
+            # --max-seconds bounds this segment (a resumed run's earlier segments are not counted)
+            return not (args.max_seconds and time.perf_counter() - t_seg > args.max_seconds)
 
     def log(st):
         if "timesteps" in st:
