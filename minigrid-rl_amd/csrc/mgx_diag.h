@@ -45,13 +45,16 @@
 #ifndef MGX_MT_WG1          // MT window groups per refill lane at S <= 8 (8 or 16; 16 for larger grids)
 #define MGX_MT_WG1 8
 #endif
+#ifndef MGX_ROLL_VMKEEP      // fused rollout's two per-step barriers: -1 __syncthreads (waits for every store),
+#define MGX_ROLL_VMKEEP -1  // N >= 0: LDS complete, <= N vector-memory ops of the wave in flight, s_barrier
+#endif
 #ifndef MGX_ROLL_S8         // 1: S = 8 runs the rollout kernel compiled for S = 8 (0: the generic one)
 #define MGX_ROLL_S8 1
 #endif
 #ifndef MGX_REFILL_S8        // 1: S = 8 refills with the kernel compiled for S = 8 (0: the generic multi one)
 #define MGX_REFILL_S8 1
 #endif
-#ifndef MGX_REFILL_EPW       // envs per S = 8 refill wave: 0 auto (32 when 64-env waves leave SIMDs idle), 32, 64
+#ifndef MGX_REFILL_EPW       // envs per S = 8 refill wave: 0 auto (32 when 64-env waves leave SIMDs idle), 16, 32, 64
 #define MGX_REFILL_EPW 0
 #endif
 #ifndef MGX_ROLLOUT_FIRST    // 1: mgx_rollout_compact enqueues its rollout before the epoch's refill (0: after;

@@ -461,6 +461,18 @@ __device__ __forceinline__ void sync_lds() {
 #endif
 }
 
+// The fused rollout's per-step barriers (MGX_ROLL_VMKEEP >= 0): LDS complete, at most N of this wave's vector
+// memory operations still in flight (its row / output stores: nothing in the launch reads them back), then
+// the barrier.  -1: __syncthreads(), a workgroup fence that waits for every store of the step.
+template <int N>
+__device__ __forceinline__ void sync_keep_vm() {
+    if constexpr (N < 0) {
+        __syncthreads();
+    } else {
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+    }
+}
+
 // =============================================================== step kernel
 // Grids in the step kernel's LDS are chunk-major, [GS/16][64 lanes][16 B] (the LDS-DMA
 // layout: one 16-B chunk per lane per global_load_lds); byte b of lane le's grid:
@@ -1309,7 +1321,8 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 const uint32_t nh = s_nh[tb ^ 1][lanev];
                 if (nh != NO_POP && (rpos_t)(s_pub[lanev] - nh) > 1) stage((rpos_t)(nh + 1));
             }
-            __syncthreads();                                   // A
+            // A: its loads (next step's actions and episodes) need not have landed yet
+            if (MGX_ROLL_VMKEEP >= 0) sync_keep_vm<63>(); else __syncthreads();
             if (s_tmask) {
                 __syncthreads();
                 if (VIS) __syncthreads();
@@ -1405,7 +1418,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 if (lanev == 0) s_tmask = tm;
             }
             RSTAMP(1);                                     // step logic (wave 0)
-            __syncthreads();
+            sync_keep_vm<MGX_ROLL_VMKEEP>();
             RSTAMP(2);                                     // wait for the block
             // (every barrier below is matched by the DMA wave's loop)
             const int le = tidv >> 2, q = tidv & 3;
@@ -1462,7 +1475,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 if (tt < rem)
                     reinterpret_cast<uint32_t *>(dst + nb16)[tt] = reinterpret_cast<const uint32_t *>(src + nb16)[tt];
             }
-            __syncthreads();                               // B
+            sync_keep_vm<MGX_ROLL_VMKEEP>();               // B
             RSTAMP(4);                                     // rows out + the block barrier
         }
     }
@@ -1880,9 +1893,10 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     unsigned long long cs = 0;
     if (tid < SLIDE_ENVS / 64) {
         const int64_t b = e0 / 64 + tid;
-        if (b < p.nblk)
-            cs = p.refill_epw == 32 ? p.blk[2 * p.nblk + 2 * b].x + p.blk[2 * p.nblk + 2 * b + 1].x
-                                    : p.blk[2 * p.nblk + b].x;
+        if (b < p.nblk) {
+            const int per = 64 / p.refill_epw;                // refill waves per 64 envs (1, 2 or 4)
+            for (int k = 0; k < per; k++) cs += p.blk[2 * p.nblk + per * b + k].x;
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long o = __shfl_xor(mn, off), q = __shfl_xor(mx, off);
@@ -2633,14 +2647,15 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         // 1,024 SIMDs); MGX_REFILL_EPW forces 32 or 64
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-        p.refill_epw = MGX_REFILL_EPW == 32 || MGX_REFILL_EPW == 64 ? MGX_REFILL_EPW : (p.nblk < 4 * cus ? 32 : 64);
+        p.refill_epw = MGX_REFILL_EPW == 16 || MGX_REFILL_EPW == 32 || MGX_REFILL_EPW == 64 ? MGX_REFILL_EPW
+                                                                                       : (p.nblk < 4 * cus ? 32 : 64);
     }
     {
-        // sections: [0, nblk) steps, [nblk, 2 nblk) fixup, [2 nblk, 4 nblk) refill waves (two per 64 envs
-        // with 32-env waves)
-        hipError_t e = hipMalloc(&h->allocs[13], (size_t)4 * p.nblk * sizeof(ulonglong4));
+        // sections: [0, nblk) steps, [nblk, 2 nblk) fixup, [2 nblk, 6 nblk) refill waves (64 / refill_epw
+        // per 64 envs)
+        hipError_t e = hipMalloc(&h->allocs[13], (size_t)6 * p.nblk * sizeof(ulonglong4));
         if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc stats"));
-        e = hipMemset(h->allocs[13], 0, (size_t)4 * p.nblk * sizeof(ulonglong4));
+        e = hipMemset(h->allocs[13], 0, (size_t)6 * p.nblk * sizeof(ulonglong4));
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset stats"));
         p.blk = (ulonglong4 *)h->allocs[13];
     }
@@ -2697,6 +2712,10 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
     h->ext = cfg->obstacles || cfg->problem == MGX_PROBLEM_FULL || cfg->problem == MGX_PROBLEM_DRP ||
              cfg->problem == MGX_PROBLEM_MOV;
+    // fewer envs per refill wave only where the S = 8 refill kernel runs (launch_refill); every other refill
+    // kernel is 64 envs per wave, and the slide reads its stats by that count
+    if (!(MGX_REFILL_S8 && h->refill_multi && !h->ext && p.problem == MGX_PROBLEM_MULTI && h->nw == 1 && S == 8))
+        p.refill_epw = 64;
 #define MGX_SET_LDS1(K, bytes) \
     HIP_TRY(hipFuncSetAttribute((const void *)K, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes)))
 #define MGX_SET_LDS(K, bytes)                                                                  \
@@ -2709,6 +2728,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     MGX_SET_LDS1(mgx_refill_multi_kernel<4>, h->lds_refill);
     MGX_SET_LDS1(mgx_refill_s8_kernel<64>, h->lds_refill);
     MGX_SET_LDS1(mgx_refill_s8_kernel<32>, h->lds_refill);
+    MGX_SET_LDS1(mgx_refill_s8_kernel<16>, h->lds_refill);
     MGX_SET_LDS(mgx_fixup_kernel, h->lds_refill);
     MGX_SET_LDS(mgx_scene_kernel, h->lds_refill);
 #undef MGX_SET_LDS
@@ -2772,6 +2792,9 @@ static mgx_status launch_refill(mgx_handle *h, void *stream, hipEvent_t done = n
         if (MGX_REFILL_S8 && h->nw == 1 && h->kp.S == 8) {
             if (h->kp.refill_epw == 32)
                 hipLaunchKernelGGL(mgx_refill_s8_kernel<32>, dim3((unsigned)((h->kp.n + 31) / 32)), b, h->lds_refill,
+                                   (hipStream_t)stream, h->kp);
+            else if (h->kp.refill_epw == 16)
+                hipLaunchKernelGGL(mgx_refill_s8_kernel<16>, dim3((unsigned)((h->kp.n + 15) / 16)), b, h->lds_refill,
                                    (hipStream_t)stream, h->kp);
             else
                 hipLaunchKernelGGL(mgx_refill_s8_kernel<64>, g, b, h->lds_refill, (hipStream_t)stream, h->kp);
@@ -3171,10 +3194,10 @@ mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]) {
     if (!h || !out) return fail(MGX_ERR_INVALID, "null argument");
     HIP_TRY(hipStreamSynchronize(h->side));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    std::vector<ulonglong4> b((size_t)4 * h->kp.nblk);
+    std::vector<ulonglong4> b((size_t)6 * h->kp.nblk);
     HIP_TRY(hipMemcpy(b.data(), h->kp.blk, b.size() * sizeof(ulonglong4), hipMemcpyDeviceToHost));
     uint64_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // blk sections: [0, nblk) step kernel (x steps, y resets), [nblk, 2 nblk) fixup, [2 nblk, 4 nblk)
+    // blk sections: [0, nblk) step kernel (x steps, y resets), [nblk, 2 nblk) fixup, [2 nblk, 6 nblk)
     // refill (x: that wave's consumption at its last launch, not a counter); z live-locks and w max MT cursor
     // in every section
     for (size_t i = 0; i < b.size(); i++) {

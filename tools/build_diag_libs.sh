@@ -19,7 +19,11 @@ declare -A V=(
   [rollfirst]="-DMGX_ROLLOUT_FIRST=1"
   [epw64]="-DMGX_REFILL_EPW=64"
   [epw32]="-DMGX_REFILL_EPW=32"
+  [epw16]="-DMGX_REFILL_EPW=16"
   [prio3]="-DMGX_REFILL_PRIO=3"
+  [vm0]="-DMGX_ROLL_VMKEEP=0"
+  [vm6]="-DMGX_ROLL_VMKEEP=6"
+  [vm12]="-DMGX_ROLL_VMKEEP=12"
   [topup4]="-DMGX_MT_TOPUP=4"
   [topup2]="-DMGX_MT_TOPUP=2"
   [r3rounds]="-DMGX_REFILL_ROUNDS=1"
