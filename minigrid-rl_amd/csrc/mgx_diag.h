@@ -48,6 +48,9 @@
 #ifndef MGX_ROLL_VMKEEP      // fused rollout's two per-step barriers: -1 __syncthreads (waits for every store),
 #define MGX_ROLL_VMKEEP -1  // N >= 0: LDS complete, <= N vector-memory ops of the wave in flight, s_barrier
 #endif
+#ifndef MGX_STEP_S8         // 1: S = 8 steps with the per-step kernel compiled for S = 8 (0: the generic one)
+#define MGX_STEP_S8 1
+#endif
 #ifndef MGX_ROLL_S8         // 1: S = 8 runs the rollout kernel compiled for S = 8 (0: the generic one)
 #define MGX_ROLL_S8 1
 #endif

@@ -613,9 +613,10 @@ __device__ __forceinline__ StepRes env_step(const EnvState &st, int a, uint8_t *
 // env's new observation is ONE 148-B row (byte 0 direction, bytes 1..147 the [c][vx][vy]
 // frame: the fast path's LDS frame row, copied out verbatim) plus its mission id byte; no
 // stack is read or rolled (mgx_gather rebuilds stacks from consecutive rows on demand).
-template <typename ActT, bool COMPACT>
+template <typename ActT, bool COMPACT, int SC = 0>   // SC > 0: the grid size as a compile-time constant
 __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, KOut o, const ActT *__restrict__ actions) {
     extern __shared__ __align__(16) uint8_t smem[];
+    const int GS = SC > 0 ? ((SC * SC + 15) & ~15) : p.GS;
     // fast path (n_stack == 4) and COMPACT: smem = frame rows [64][148] (new frame at bytes
     // 1..147); staged path: smem = image stacks [64][IMG] (new frame in slot 0 of a row).
     const bool fast = !COMPACT && p.fast_roll;
@@ -625,10 +626,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // the SB3 layout's 25.8 KB only three did, and the fourth waited for a second round
     constexpr int CSTK = (BLOCK_ENVS * FROW + 15) & ~15;
     uint8_t *s_grid = smem + (COMPACT ? CSTK : p.stk_step);   // grids, chunk-major [GS/16][64 lanes][16 B] (cm_off)
-    uint8_t *s_pgrid = s_grid + BLOCK_ENVS * p.GS;   // popped episodes' grids, same layout
+    uint8_t *s_pgrid = s_grid + BLOCK_ENVS * GS;   // popped episodes' grids, same layout
     // LDS-DMA destinations are lane-linear (kept in the dynamic segment: hipcc 7.2 emitted no
     // M0 setup for a static __shared__ destination)
-    uint4 *s_phdr = reinterpret_cast<uint4 *>(s_pgrid + BLOCK_ENVS * p.GS);   // popped ring slot header
+    uint4 *s_phdr = reinterpret_cast<uint4 *>(s_pgrid + BLOCK_ENVS * GS);   // popped ring slot header
     uint4 *s_tokA = s_phdr + BLOCK_ENVS;         // per lane: the current mission's tokens 0..15,
     uint4 *s_tokB = s_tokA + BLOCK_ENVS;         // 16..31 (envs whose stack is still filling)
     uint4 *s_ptokA = s_tokB + BLOCK_ENVS;        // ... and the popped episode's mission tokens
@@ -651,7 +652,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     const int tid = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * BLOCK_ENVS;
     const int ne = (int)min<int64_t>(BLOCK_ENVS, p.n - e0);
-    const int S = p.S;
+    const int S = SC > 0 ? SC : p.S;
     if (tid == 0) s_ll = 0;
     // issue priority over the refill's waves on the same SIMD (MGX_STEP_PRIO; wave-uniform)
     if (p.step_prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -735,8 +736,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // flight, which would serialise them.
     {
         const int lane = tid & (BLOCK_ENVS - 1);
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.grid + (e0 + min(lane, ne - 1)) * p.GS);
-        for (int c = tid >> 6; c < (p.GS >> 4); c += BLOCK_THREADS / 64)
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.grid + (e0 + min(lane, ne - 1)) * GS);
+        for (int c = tid >> 6; c < (GS >> 4); c += BLOCK_THREADS / 64)
             __builtin_amdgcn_global_load_lds(src + c, s_grid + c * (BLOCK_ENVS * 16), 16, 0, 0);
     }
     // (e) SubprocVecEnv auto-reset, speculatively.  A step can end the episode only on
@@ -772,8 +773,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
                 }
                 __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot, s_prng, 16, 0, 0);
                 __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot + 1, s_prng + BLOCK_ENVS, 16, 0, 0);
-                const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * p.GS);
-                for (int c = 0; c < (p.GS >> 4); c++)
+                const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * GS);
+                for (int c = 0; c < (GS >> 4); c++)
                     __builtin_amdgcn_global_load_lds(gsrc + c, s_pgrid + c * (BLOCK_ENVS * 16), 16, 0, 0);
             }
             // (no register load here: its phi copy after the branch would wait on the DMA above)
@@ -908,10 +909,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // area, both chunk-major), at line granularity: grids smaller than a 128-B line are written
     // for every env of a line with a dirty grid, so that no line is written in part.
     if (!(MGX_DIAG_SKIP & 16)) {
-        const int q16 = p.GS >> 4;
-        const int epl = p.GS < 128 ? 128 / p.GS : 1;          // envs per line (GS is a multiple of 16)
+        const int q16 = GS >> 4;
+        const int epl = GS < 128 ? 128 / GS : 1;          // envs per line (GS is a multiple of 16)
         const unsigned long long dirtym = s_dirtym;
-        uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * p.GS);
+        uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * GS);
         for (int i = tid; i < ne * q16; i += BLOCK_THREADS) {
             const int e = i / q16, c = i - e * q16;
             if (!((dirtym >> (e & ~(epl - 1))) & ((1ull << epl) - 1))) continue;
@@ -2689,10 +2690,14 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->lds_reset = (size_t)p.stk_lds + (size_t)p.grid_lds;
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     h->lds_step_compact = (size_t)((BLOCK_ENVS * FROW + 15) & ~15) + (size_t)BLOCK_ENVS * 2 * GS   // frame rows + grids
                           + (size_t)BLOCK_ENVS * 3 * 16;                                     // + popped header, RNG snapshot
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
     // fused rollout: frame rows + current grids + two staged ring episodes (grid, header) + actions
     // [+ 'move' target ranges]
     h->lds_rollout = (size_t)((BLOCK_ENVS * FROW + 15) & ~15) + (size_t)BLOCK_ENVS * 3 * GS +
@@ -2956,12 +2961,16 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
         mgx_status ps = publish_for_steps(h, stream);
         if (ps != MGX_OK) return ps;
     }
-    if (action_bytes == 4)
-        hipLaunchKernelGGL((mgx_step_kernel<int32_t, false>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
-                           (hipStream_t)stream, h->kp, o, (const int32_t *)actions_dev);
-    else if (action_bytes == 8)
-        hipLaunchKernelGGL((mgx_step_kernel<int64_t, false>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step,
-                           (hipStream_t)stream, h->kp, o, (const int64_t *)actions_dev);
+    // S = 8 (configs 2, 3 and 4): the kernel compiled for the grid size (MGX_STEP_S8)
+#define MGX_STEP(A, C, SCV, LDS)                                                                                   \
+    hipLaunchKernelGGL((mgx_step_kernel<A, C, SCV>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), LDS, (hipStream_t)stream, \
+                       h->kp, o, (const A *)actions_dev)
+    const bool s8 = MGX_STEP_S8 && h->kp.S == 8;
+    if (action_bytes == 4) {
+        if (s8) MGX_STEP(int32_t, false, 8, h->lds_step); else MGX_STEP(int32_t, false, 0, h->lds_step);
+    } else if (action_bytes == 8) {
+        if (s8) MGX_STEP(int64_t, false, 8, h->lds_step); else MGX_STEP(int64_t, false, 0, h->lds_step);
+    }
     HIP_TRY(hipGetLastError());
     if (h->kp.D == 0) {   // no ring: every done env is generated inline, right after the step
         mgx_status ss = launch_slide(h, stream);
@@ -3003,12 +3012,13 @@ mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_b
     }
     mgx_status ps = publish_for_steps(h, stream);
     if (ps != MGX_OK) return ps;
-    if (action_bytes == 4)
-        hipLaunchKernelGGL((mgx_step_kernel<int32_t, true>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step_compact,
-                           (hipStream_t)stream, h->kp, o, (const int32_t *)actions_dev);
-    else
-        hipLaunchKernelGGL((mgx_step_kernel<int64_t, true>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), h->lds_step_compact,
-                           (hipStream_t)stream, h->kp, o, (const int64_t *)actions_dev);
+    const bool s8 = MGX_STEP_S8 && h->kp.S == 8;
+    if (action_bytes == 4) {
+        if (s8) MGX_STEP(int32_t, true, 8, h->lds_step_compact); else MGX_STEP(int32_t, true, 0, h->lds_step_compact);
+    } else {
+        if (s8) MGX_STEP(int64_t, true, 8, h->lds_step_compact); else MGX_STEP(int64_t, true, 0, h->lds_step_compact);
+    }
+#undef MGX_STEP
     HIP_TRY(hipGetLastError());
     h->calls++;
     return MGX_OK;

@@ -10,6 +10,7 @@ declare -A V=(
   [rstamps_serial]="-DMGX_RSTAMPS=1 -DMGX_SERIAL_REFILL=1"
   [rclock]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1"
   [nos8]="-DMGX_ROLL_S8=0"
+  [nostep8]="-DMGX_STEP_S8=0"
   [skip1]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=1"
   [skip2]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=2"
   [skip4]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=4"
@@ -23,6 +24,8 @@ declare -A V=(
   [prio3]="-DMGX_REFILL_PRIO=3"
   [vm0]="-DMGX_ROLL_VMKEEP=0"
   [vm6]="-DMGX_ROLL_VMKEEP=6"
+  [vm4]="-DMGX_ROLL_VMKEEP=4"
+  [vm8]="-DMGX_ROLL_VMKEEP=8"
   [vm12]="-DMGX_ROLL_VMKEEP=12"
   [topup4]="-DMGX_MT_TOPUP=4"
   [topup2]="-DMGX_MT_TOPUP=2"
