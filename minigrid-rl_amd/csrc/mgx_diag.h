@@ -46,8 +46,8 @@
 #define MGX_MT_WG1 8
 #endif
 #ifndef MGX_ROLL_VMKEEP      // fused rollout's two per-step barriers: -1 __syncthreads (waits for every store),
-#define MGX_ROLL_VMKEEP -1  // N >= 0: LDS complete, <= N vector-memory ops of the wave in flight, s_barrier
-#endif
+#define MGX_ROLL_VMKEEP 8   // N >= 0: LDS complete, <= N vector-memory ops of the wave in flight, s_barrier
+#endif                      // (round 4 A/B: default line +8-10 % at 8 or 12, 20-step line within noise)
 #ifndef MGX_STEP_S8         // 1: S = 8 steps with the per-step kernel compiled for S = 8 (0: the generic one)
 #define MGX_STEP_S8 1
 #endif
