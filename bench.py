@@ -638,7 +638,7 @@ def measure_rollout(args, layout, world, rank, dev):
         # shape (profiles/r04_pmc/kernel_stats_<cfg>_<layout>_e<E>.csv): `frac` recomputed from profiles/
         kstat = _rocprof_kernel_avg(os.path.join(ROOT, "profiles", "r04_pmc", "kernel_stats_%d_%s_e%d.csv" % (
             args.config, layout, spl if fused else E)), "mgx_rollout_kernel" if fused else
-            ("mgx_step_kernel<int, true>" if compact else "mgx_step_kernel<int, false>"))
+            ("mgx_step_kernel<int, true" if compact else "mgx_step_kernel<int, false"))   # (<..., 8>: the S = 8 instance)
         # VecFrameStack image + direction roll (reported separately); the compact layout rolls nothing
         stack_bytes = 0 if compact else n * (441 + 588 + 12 + 16)
         out = {
@@ -678,8 +678,8 @@ def measure_rollout(args, layout, world, rank, dev):
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": ("mgx_rollout_kernel<false> (fused: %d steps per launch; per-step figures = "
                                     "launch / %d)" % (E, E) if fused else
-                                    "mgx_step_kernel<int, true> (compact)" if compact else
-                                    "mgx_step_kernel<int, false> (SB3 stacks)"),
+                                    "mgx_step_kernel<int, true[, 8]> (compact)" if compact else
+                                    "mgx_step_kernel<int, false[, 8]> (SB3 stacks)"),
                          "avg_launch_us": per_launch_s * 1e6,
                          "rocprof": None if kstat is None else {
                              "source": kstat["source"], "avg_launch_us": kstat["avg_us"] / spl,

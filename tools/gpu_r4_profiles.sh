@@ -24,7 +24,7 @@ for shape in ${SHAPES:-2:fused:20 2:fused:2048 2:compact:20 4:fused:2048 5:fused
   grep '^{"metric"' $O/s_$tag.log > $O/bench_$tag.json || true
   timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $O/f_$tag -o run -- python3 $B > $O/f_$tag.log 2>&1 || { tail -20 $O/f_$tag.log; exit 1; }
   timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $O/w_$tag -o run -- python3 $B > $O/w_$tag.log 2>&1 || { tail -20 $O/w_$tag.log; exit 1; }
-  if [ $lay = fused ]; then K=mgx_rollout_kernel; SPL=$E; else K="mgx_step_kernel<int, true>"; SPL=1; fi
+  if [ $lay = fused ]; then K=mgx_rollout_kernel; SPL=$E; else K="mgx_step_kernel<int, true"; SPL=1; fi
   python3 $R/tools/pmc_summary.py $(find $O/f_$tag -name '*counter_collection.csv' | head -1) $(find $O/w_$tag -name '*counter_collection.csv' | head -1) "$K" ${N[$cfg]} ${S[$cfg]} ${M[$cfg]} $SPL $O/pmc_$tag.json
   python3 $R/tools/pmc_summary.py $(find $O/f_$tag -name '*counter_collection.csv' | head -1) $(find $O/w_$tag -name '*counter_collection.csv' | head -1) "mgx_refill" ${N[$cfg]} ${S[$cfg]} ${M[$cfg]} $E $O/pmc_refill_$tag.json
   rm -rf $O/s_$tag $O/f_$tag $O/w_$tag
