@@ -355,6 +355,23 @@ def _rocprof_kernel_avg(path, kernel):
     return None
 
 
+def _rocprof_trace_timed_avg(path, kernel, first, count):
+    """Average duration (us) of launches [first, first + count) of `kernel` (name substring, in start order) in a
+    committed rocprofv3 kernel trace (.csv.gz) of this same command: the timed region's launches (after the
+    warm-up's, the untimed graph replay's), or None."""
+    import csv
+    import gzip
+    try:
+        rows = [r for r in csv.DictReader(gzip.open(path, "rt")) if kernel in r.get("Kernel_Name", "")]
+    except OSError:
+        return None
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    sel = rows[first:first + count]
+    if len(sel) != count or count == 0:
+        return None
+    return sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in sel) / 1e3 / count
+
+
 def pick_epoch(K, D=256):
     """Refill epoch E (mgx refill_every) so that the K timed steps are whole epochs: the largest
     divisor of K in [8, min(64, D/4)] (at D/2 the ring invariant 2E <= D makes every epoch refill the
@@ -639,6 +656,15 @@ def measure_rollout(args, layout, world, rank, dev):
         kstat = _rocprof_kernel_avg(os.path.join(ROOT, "profiles", "r04_pmc", "kernel_stats_%d_%s_e%d.csv" % (
             args.config, layout, spl if fused else E)), "mgx_rollout_kernel" if fused else
             ("mgx_step_kernel<int, true" if compact else "mgx_step_kernel<int, false"))   # (<..., 8>: the S = 8 instance)
+        # ... and over the timed region's launches alone, from the committed kernel trace of the same command:
+        # in the timed graph replays the epoch's refill is dispatched ahead of the rollout and the kernel runs
+        # longer than in the eager probe windows above
+        kname = "mgx_rollout_kernel" if fused else ("mgx_step_kernel<int, true" if compact else "mgx_step_kernel<int, false")
+        per = E if fused else 1                                  # steps per launch
+        t_avg = _rocprof_trace_timed_avg(os.path.join(ROOT, "profiles", "r04_pmc", "kernel_trace_%d_%s_e%d.csv.gz" % (
+            args.config, layout, spl if fused else E)), kname, (W + (K if graphs else 0)) // per, K // per)
+        if kstat is not None and t_avg is not None:
+            kstat["timed_avg_us"] = t_avg
         # VecFrameStack image + direction roll (reported separately); the compact layout rolls nothing
         stack_bytes = 0 if compact else n * (441 + 588 + 12 + 16)
         out = {
@@ -685,7 +711,13 @@ def measure_rollout(args, layout, world, rank, dev):
                              "source": kstat["source"], "avg_launch_us": kstat["avg_us"] / spl,
                              "frac": b_alg / (kstat["avg_us"] / spl * 1e-6) / 1e9 / PEAK_HBM_GBPS,
                              "note": "the committed rocprofv3 --stats average of the same kernel at this config and "
-                                     "launch shape (per step), B_alg of this run"},
+                                     "launch shape (per step; all its launches: warm-up, graph replays, probe), "
+                                     "B_alg of this run",
+                             "timed_avg_us": (kstat["timed_avg_us"] / spl) if "timed_avg_us" in kstat else None,
+                             "timed_frac": (b_alg / (kstat["timed_avg_us"] / spl * 1e-6) / 1e9 / PEAK_HBM_GBPS)
+                             if "timed_avg_us" in kstat else None,
+                             "timed_note": "the timed region's launches alone (committed kernel trace of the same "
+                                           "command, per step): the graph replays, refill dispatched first"},
                          "probe_launches": len(probe_us),
                          "step_pipeline_us": float(gpu_ms) * 1e3 / K,
                          "alg_bytes_per_launch": b_alg, "resets_per_launch": resets_per_launch,
