@@ -27,3 +27,25 @@ def test_pick_horizon():
     for K, E in ((2048, 32), (96, 32), (20, 20), (640, 32)):
         H = bench.pick_horizon(K, E, 0)
         assert K % H == 0 and H % E == 0 and H <= 1024
+
+
+def test_committed_profiles_reproduce_the_driver_line_roofline():
+    """profiles/r04_pmc holds, for the driver's command (config 2, fused, 20-step epochs), the rocprofv3
+    kernel stats, the kernel trace and the FETCH / WRITE passes that bench.py reads back: the rollout
+    kernel's average launch, the timed region's launch (after 13 warm-up epochs and the graph's untimed
+    replay) and the PMC bytes per launch of the same launch shape."""
+    import json
+    d = os.path.join(bench.ROOT, "profiles", "r04_pmc")
+    st = bench._rocprof_kernel_avg(os.path.join(d, "kernel_stats_2_fused_e20.csv"), "mgx_rollout_kernel")
+    assert st is not None and st["calls"] >= 15 and 80.0 < st["avg_us"] < 250.0
+    W, K, E = 260, 20, 20                      # bench's warm-up (>= 256, whole epochs), timed steps, epoch
+    t = bench._rocprof_trace_timed_avg(os.path.join(d, "kernel_trace_2_fused_e20.csv.gz"), "mgx_rollout_kernel",
+                                       (W + K) // E, K // E)
+    assert t is not None and 80.0 < t < 300.0
+    pmc = json.load(open(os.path.join(d, "pmc_2_fused_e20.json")))
+    assert pmc["steps_per_launch"] == 20 and pmc["n_envs"] == 65536 and pmc["mission"] == 5
+    # the rows (148 B), mission ids, rewards and flags the launch writes: >= 20 x 65,536 x 158 B
+    assert pmc["write_bytes_per_launch"] >= 20 * 65536 * 158
+    # a window of launches outside the trace is refused, not averaged
+    assert bench._rocprof_trace_timed_avg(os.path.join(d, "kernel_trace_2_fused_e20.csv.gz"),
+                                          "mgx_rollout_kernel", 10 ** 6, 1) is None
