@@ -51,6 +51,9 @@
 #ifndef MGX_STEP_S8         // 1: S = 8 steps with the per-step kernel compiled for S = 8 (0: the generic one)
 #define MGX_STEP_S8 1
 #endif
+#ifndef MGX_ROLL_DEFER_ROWS  // 1: fused rollout copies step t's rows out during step t + 1's logic (waves 1-3)
+#define MGX_ROLL_DEFER_ROWS 1
+#endif
 #ifndef MGX_ROLL_S8         // 1: S = 8 runs the rollout kernel compiled for S = 8 (0: the generic one)
 #define MGX_ROLL_S8 1
 #endif

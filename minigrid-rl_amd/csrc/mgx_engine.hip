@@ -1338,9 +1338,27 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             __syncthreads();                                   // B: ... before the next step reads them
         }
     } else {
+        // MGX_ROLL_DEFER_ROWS: step t's frame rows are copied out by waves 1-3 during step t + 1's logic (wave 0
+        // alone), before its post-logic barrier, instead of by every wave at the end of step t: the copy-out
+        // leaves the step's critical path (the last step's rows after the loop).  s_stk is rewritten only after
+        // that barrier (terminal rows, render).
+        const auto rows_out_block = [&](int t_rows, int tt, int nt) {
+            const int nb16 = (ne * FROW) >> 4;
+            const uint4 *src = reinterpret_cast<const uint4 *>(s_stk);
+            uint4 *dst = reinterpret_cast<uint4 *>(o.rows + ((int64_t)t_rows * N + e0) * FROW);
+            for (int i = tt; i < nb16; i += nt) dst[i] = src[i];
+            const int rem = ((ne * FROW) >> 2) - (nb16 << 2);
+            if (tt < rem)
+                reinterpret_cast<uint32_t *>(dst + nb16)[tt] = reinterpret_cast<const uint32_t *>(src + nb16)[tt];
+        };
         for (int t = 0; t < K; t++) {
             const int tb = t & 1;
             RSTAMP(0);
+            if (MGX_ROLL_DEFER_ROWS && t > 0 && !wave0) {
+                int tq = tid;
+                asm volatile("" : "+v"(tq));
+                rows_out_block(t - 1, tq - BLOCK_ENVS, BLOCK_THREADS - BLOCK_ENVS);
+            }
             // thread index through an opaque copy: lane- / env-derived addresses are then computed inside
             // each region of the step, instead of being hoisted out of the loop and kept live through all of
             // them (96 -> fewer VGPRs; the render's and the step logic's registers no longer add up)
@@ -1461,7 +1479,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 __syncthreads();
             }
             RSTAMP(3);                                     // terminal rows + render
-            {
+            if (!MGX_ROLL_DEFER_ROWS) {
                 // rows out: per wave (its 16 rows, no barrier) or, after process_vis, per block
                 const bool wave_rows = !VIS;
                 const int r0 = wave_rows ? (tidv >> 6) * 16 : 0;
@@ -1479,6 +1497,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             sync_keep_vm<MGX_ROLL_VMKEEP>();               // B
             RSTAMP(4);                                     // rows out + the block barrier
         }
+        if (MGX_ROLL_DEFER_ROWS && K > 0) rows_out_block(K - 1, tid, BLOCK_THREADS);   // the last step's rows
     }
 #if MGX_RSTAMPS
     if (tid == 0)

@@ -23,6 +23,7 @@ declare -A V=(
   [epw16]="-DMGX_REFILL_EPW=16"
   [prio3]="-DMGX_REFILL_PRIO=3"
   [vmsync]="-DMGX_ROLL_VMKEEP=-1"
+  [nodefer]="-DMGX_ROLL_DEFER_ROWS=0"
   [vm0]="-DMGX_ROLL_VMKEEP=0"
   [vm6]="-DMGX_ROLL_VMKEEP=6"
   [vm4]="-DMGX_ROLL_VMKEEP=4"
