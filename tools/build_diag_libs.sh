@@ -29,6 +29,7 @@ declare -A V=(
   [vm4]="-DMGX_ROLL_VMKEEP=4"
   [vm8]="-DMGX_ROLL_VMKEEP=8"
   [vm12]="-DMGX_ROLL_VMKEEP=12"
+  [vm16]="-DMGX_ROLL_VMKEEP=16"
   [topup4]="-DMGX_MT_TOPUP=4"
   [topup2]="-DMGX_MT_TOPUP=2"
   [r3rounds]="-DMGX_REFILL_ROUNDS=1"
@@ -39,6 +40,7 @@ names=("$@")
 [ ${#names[@]} -eq 0 ] && names=("${!V[@]}")
 pids=()
 for n in "${names[@]}"; do
+  [ -n "${V[$n]+x}" ] || { echo "unknown variant: $n"; exit 1; }
   make -s -B EXTRA="${V[$n]}" OUT=mgx/libmgx_$n.so > /tmp/build_diag_$n.log 2>&1 &
   pids+=($!)
   while [ $(jobs -rp | wc -l) -ge 4 ]; do sleep 1; done
