@@ -1891,22 +1891,36 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     MtCtl *c = p.mtc;
     unsigned long long mn = ~0ull, mx = 0;
     const int64_t e0 = (int64_t)blockIdx.x * SLIDE_ENVS;
-#pragma unroll 4
-    for (int k = 0; k < SLIDE_ENVS / SLIDE_THREADS; k++) {
+    // Every load of the thread's 16 envs first, then the stores: with a store between them (the ring_pubn copy)
+    // each load group also waited for the store before it (vmcnt counts both on gfx9) -- 16 store round trips
+    // per thread (round 4).
+    constexpr int EPT = SLIDE_ENVS / SLIDE_THREADS;
+    rpos_t tl[EPT];
+    unsigned long long cu[EPT], pc[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; k++) {
+        const int64_t e = e0 + k * SLIDE_THREADS + tid;
+        const bool in = e < p.n;
+        const int64_t ec = in ? e : 0;
+        tl[k] = p.D > 0 ? p.ring_tail[ec] : (rpos_t)0;
+        const uint2 cr = reinterpret_cast<const uint2 *>(p.cur_rng + 2 * ec + 1)[1];   // .z, .w: the MT cursor
+        const uint2 ax = reinterpret_cast<const uint2 *>(p.aux + ec)[1];             // producer cursor
+        cu[k] = in ? ((unsigned long long)cr.x | ((unsigned long long)cr.y << 32)) : ~0ull;
+        pc[k] = in ? ((unsigned long long)ax.x | ((unsigned long long)ax.y << 32)) : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; k++) {
         const int64_t e = e0 + k * SLIDE_THREADS + tid;
         if (e < p.n) {
-            if (p.D > 0) p.ring_pubn[e] = p.ring_tail[e];   // the refill before this slide has completed
-            const uint4 cr = p.cur_rng[2 * e + 1];
-            unsigned long long v = (unsigned long long)cr.z | ((unsigned long long)cr.w << 32);
+            if (p.D > 0) p.ring_pubn[e] = tl[k];           // the refill before this slide has completed
+            unsigned long long v = cu[k];
             if (p.start_rng) {
                 const uint4 sr = p.start_rng[2 * e + 1];
                 const unsigned long long u = (unsigned long long)sr.z | ((unsigned long long)sr.w << 32);
                 v = u < v ? u : v;
             }
             mn = v < mn ? v : mn;
-            const uint4 ax = p.aux[e];                        // producer cursor (mgx_refill_kernel)
-            const unsigned long long w = (unsigned long long)ax.z | ((unsigned long long)ax.w << 32);
-            mx = w > mx ? w : mx;
+            mx = pc[k] > mx ? pc[k] : mx;
         }
     }
     // the refill waves' consumption (mgx_refill_kernel writes it in its workgroup stats): one per 64 envs
