@@ -79,6 +79,11 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
     ap.add_argument("--probe", type=int, default=256, help="eager steps timed per launch for the roofline")
     ap.add_argument("--workload", default="rollout", choices=["rollout", "ppo"])
+    ap.add_argument("--gae-fused", type=int, default=0,
+                    help="fused layout with one launch per horizon (E = H): 1 = GAE in the rollout launch "
+                         "(mgx_rollout_compact_gae); 0 = a separate mgx_gae_dones launch (default: the same "
+                         "speed on the driver's line in round 4's A/B, and the separate kernel is the one the "
+                         "per-step layouts use)")
     ap.add_argument("--refill-every", type=int, default=0, help="steps per refill epoch (0 = engine default, D/4)")
     ap.add_argument("--min-warmup", type=int, default=256,
                     help="rollout: the warm-up is at least this many steps (whole refill epochs)")
@@ -497,7 +502,11 @@ def measure_rollout(args, layout, world, rank, dev):
         if compact:
             if c:
                 cbuf.carry_over()
-            if fused:                                    # one launch per refill epoch
+            if fused and E == H and args.gae_fused:      # one launch for the horizon, its GAE fused in
+                cbuf.rollout(0, actions[W + c * H:W + c * H + E], gae=dict(
+                    values=vals, last_values=last_v, gamma=gamma, gae_lambda=lam, out=(adv, ret), stats=hist[c],
+                    scratch=scratch))
+            elif fused:                                  # one launch per refill epoch
                 for j in range(0, H, E):
                     cbuf.rollout(j, actions[W + c * H + j:W + c * H + j + E])
             else:
@@ -506,7 +515,8 @@ def measure_rollout(args, layout, world, rank, dev):
         else:
             for j in range(H):
                 eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
-        gae_dones(rew, vals, dones, last_v, gamma, lam, stats=hist[c], scratch=scratch, out=(adv, ret))
+        if not (fused and E == H and args.gae_fused):
+            gae_dones(rew, vals, dones, last_v, gamma, lam, stats=hist[c], scratch=scratch, out=(adv, ret))
         eng.join()                                       # the epoch's refill (it ran beside GAE): the
                                                          # chunk's graph is self-contained, and the region
                                                          # pays for every refill it forked
@@ -693,9 +703,11 @@ def measure_rollout(args, layout, world, rank, dev):
                        "problem": args.problem, "mission": mission, "size": args.size, "num_objects": 4,
                        "envs_per_gpu": n, "n_stack": args.n_stack, "parallelism": "env-sharded dp%d" % world,
                        "hipgraph": bool(graphs), "refill_every": E, "horizon": H, "layout": layout,
-                       "timed": "%d steps = %d whole refill epochs%s; GAE + adv-stat %s every %d steps" % (
+                       "timed": "%d steps = %d whole refill epochs%s; GAE + adv-stat %s every %d steps%s" % (
                            K, K // E, "" if aligned else " + a joined partial one",
-                           "all-reduce (%s)" % dist.get_backend() if world > 1 else "accumulation", H)},
+                           "all-reduce (%s)" % dist.get_backend() if world > 1 else "accumulation", H,
+                           " (fused into the rollout launch: mgx_rollout_compact_gae)" if fused and E == H and args.gae_fused
+                           else "")},
             "window": {"refill_launches": forks if forks is not None else st1["refill_launches"] - st0["refill_launches"],
                        "episodes_produced": (st1["resets"] - st0["resets"]) + (st1["queued"] - st0["queued"]),
                        "episodes_consumed": st1["resets"] - st0["resets"],

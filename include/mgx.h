@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MGX_ABI_VERSION 4
+#define MGX_ABI_VERSION 5
 
 /* Live-lock cap (engine policy; the reference hangs): a
  * reset attempt may consume at most this many MT19937 words; the attempt that
@@ -257,6 +257,25 @@ mgx_status mgx_gae_dones(const float *rewards_dev, const float *values_dev, cons
                          const float *last_values_dev, int64_t T, int64_t N, float gamma, float gamma_lambda,
                          float *advantages_dev, float *returns_dev, double *adv_stats_dev,
                          double *stats_scratch_dev, void *stream);
+
+/* mgx_rollout_compact followed by mgx_gae_dones over the K steps it runs (its rewards_dev and dones_dev,
+ * T = K), the GAE fused into the launch: each workgroup runs the recurrence of its 64 envs as soon as its
+ * own K steps are done, reading back the rewards and dones it wrote (no second kernel over the rollout).
+ * Same fp32 op order and outputs as mgx_gae_dones (bit for bit); adv_stats_dev / stats_scratch_dev as
+ * there (the fold of the per-workgroup partials is a second, one-workgroup launch).  Replaces the
+ * reference's collect_rollouts + compute_returns_and_advantage pair for a rollout whose actions are
+ * known up front and whose horizon is this launch (ppo.py:159; SB3 OnPolicyAlgorithm.collect_rollouts). */
+typedef struct mgx_gae_args {
+    const float *values_dev;       /* f32 [K][N] */
+    const float *last_values_dev;  /* f32 [N]: V(observation after step K-1) */
+    float gamma, gamma_lambda;     /* gamma_lambda = float(gamma * gae_lambda), as mgx_gae_dones */
+    float *advantages_dev;         /* f32 [K][N] */
+    float *returns_dev;            /* f32 [K][N] */
+    double *adv_stats_dev;         /* f64 [3] (optional) */
+    double *stats_scratch_dev;     /* f64 [MGX_GAE_SCRATCH_WORDS] (optional) */
+} mgx_gae_args;
+mgx_status mgx_rollout_compact_gae(mgx_handle *h, const int32_t *actions_dev, int K, const mgx_rollout_out *out,
+                                   const mgx_gae_args *gae, void *stream);
 
 /* Scene record of env `env`'s current episode, for PlaygroundEnv.llm_description /
  * LLMDescriptionWrapper (environment.py:152-195; manual mode, one env): the episode is

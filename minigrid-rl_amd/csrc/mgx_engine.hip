@@ -1187,6 +1187,11 @@ struct ROut {
     uint8_t *term, *trunc, *done;    // [K][N]
     float *ep_ret;                   // [N] as after the last step (optional)
     int32_t *ep_len, *livelock;      // [N] as after the last step (optional)
+    // mgx_rollout_compact_gae: GAE of the launch's K steps in the epilogue (gadv null: none)
+    const float *gv, *glv;           // values [K][N], last values [N]
+    float gg, gc;                    // gamma, float(gamma * lambda)
+    float *gadv, *gret;              // [K][N]
+    double *gshard;                  // (sum A, sum A^2) partials (GAE_SHARDS x 2), or null
 };
 constexpr int ROLL_THREADS = BLOCK_THREADS + 64;
 
@@ -1498,6 +1503,52 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             RSTAMP(4);                                     // rows out + the block barrier
         }
         if (MGX_ROLL_DEFER_ROWS && K > 0) rows_out_block(K - 1, tid, BLOCK_THREADS);   // the last step's rows
+        if (o.gadv && wave0) {
+            // mgx_rollout_compact_gae: mgx_gae_kernel<true>'s recurrence (same fp32 op order) for this lane's
+            // env over the K steps it just ran, from the rewards / dones it wrote itself (program order), eight
+            // steps' loads in flight at a time
+            double s1 = 0.0, s2 = 0.0;
+            if (lane < ne) {
+                const int64_t col = e0 + lane;
+                float last = 0.0f, nv = o.glv[col];
+                for (int t0 = K - 1; t0 >= 0; t0 -= 8) {
+                    float rr[8], vv[8], dd[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const int t = t0 - i;
+                        const int64_t k = (int64_t)(t >= 0 ? t : 0) * N + col;
+                        rr[i] = o.reward[k];
+                        vv[i] = o.gv[k];
+                        dd[i] = (float)o.done[k];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const int t = t0 - i;
+                        if (t < 0) break;
+                        const int64_t k = (int64_t)t * N + col;
+                        const float nnt = 1.0f - dd[i];
+                        const float delta = (rr[i] + (o.gg * nv) * nnt) - vv[i];
+                        last = delta + (o.gc * nnt) * last;
+                        o.gadv[k] = last;
+                        o.gret[k] = last + vv[i];
+                        s1 += (double)last;
+                        s2 += (double)last * (double)last;
+                        nv = vv[i];
+                    }
+                }
+            }
+            if (o.gshard) {
+                for (int off = 32; off > 0; off >>= 1) {
+                    s1 += __shfl_down(s1, off);
+                    s2 += __shfl_down(s2, off);
+                }
+                if (lane == 0) {
+                    double *sh = o.gshard + 2 * (blockIdx.x & 255);   // GAE_SHARDS slots, as mgx_gae_kernel
+                    atomicAdd(&sh[0], s1);
+                    atomicAdd(&sh[1], s2);
+                }
+            }
+        }
     }
 #if MGX_RSTAMPS
     if (tid == 0)
@@ -3057,8 +3108,9 @@ mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_b
     return MGX_OK;
 }
 
-mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K, const mgx_rollout_out *out,
-                               void *stream) {
+static double *gae_scratch(double *stats_scratch_dev);
+static mgx_status rollout_impl(mgx_handle *h, const int32_t *actions_dev, int K, const mgx_rollout_out *out,
+                               const mgx_gae_args *gae, void *stream) {
     if (!h || !out || !actions_dev) return fail(MGX_ERR_INVALID, "mgx_rollout_compact: null argument");
     if (!out->rows_dev || !out->mission_ids_dev || !out->rewards_dev || !out->terminated_dev || !out->truncated_dev ||
         !out->dones_dev)
@@ -3082,6 +3134,21 @@ mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K,
     o.ep_ret = out->ep_return_dev;
     o.ep_len = out->ep_len_dev;
     o.livelock = out->livelock_dev;
+    o.gv = o.glv = nullptr;
+    o.gg = o.gc = 0.0f;
+    o.gadv = o.gret = nullptr;
+    o.gshard = nullptr;
+    if (gae) {
+        if (!gae->values_dev || !gae->last_values_dev || !gae->advantages_dev || !gae->returns_dev)
+            return fail(MGX_ERR_INVALID, "mgx_rollout_compact_gae: missing GAE buffer");
+        o.gv = gae->values_dev;
+        o.glv = gae->last_values_dev;
+        o.gg = gae->gamma;
+        o.gc = gae->gamma_lambda;
+        o.gadv = gae->advantages_dev;
+        o.gret = gae->returns_dev;
+        o.gshard = gae->adv_stats_dev ? gae_scratch(gae->stats_scratch_dev) : nullptr;
+    }
     // Launch order of the epoch's refill and this rollout (both start from the same fork point):
     // MGX_ROLLOUT_FIRST.  Refill first is the default: with the rollout first, its workgroups took the CU
     // slots and the refill's waves, the longer of the two, started late (20-step line 4.0-4.2 vs
@@ -3114,7 +3181,23 @@ mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K,
         if (fs != MGX_OK) return fs;
     }
     h->calls += (uint64_t)K;
+    if (o.gshard) {   // fold the launch's GAE partials into the caller's triple (as mgx_gae_dones)
+        hipLaunchKernelGGL(mgx_gae_reduce_kernel, dim3(1), dim3(GAE_SHARDS), 0, (hipStream_t)stream,
+                           gae->adv_stats_dev, o.gshard, (double)K * (double)h->kp.n);
+        HIP_TRY(hipGetLastError());
+    }
     return MGX_OK;
+}
+
+mgx_status mgx_rollout_compact(mgx_handle *h, const int32_t *actions_dev, int K, const mgx_rollout_out *out,
+                               void *stream) {
+    return rollout_impl(h, actions_dev, K, out, nullptr, stream);
+}
+
+mgx_status mgx_rollout_compact_gae(mgx_handle *h, const int32_t *actions_dev, int K, const mgx_rollout_out *out,
+                                   const mgx_gae_args *gae, void *stream) {
+    if (!gae) return fail(MGX_ERR_INVALID, "mgx_rollout_compact_gae: null GAE arguments");
+    return rollout_impl(h, actions_dev, K, out, gae, stream);
 }
 
 mgx_status mgx_observe_compact(mgx_handle *h, uint8_t *row_dev, uint8_t *mission_id_dev, void *stream) {

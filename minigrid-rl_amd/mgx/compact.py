@@ -83,11 +83,14 @@ class CompactBuffer:
                    "mgx_step_compact")
         e.calls += 1
 
-    def rollout(self, t, actions):
+    def rollout(self, t, actions, gae=None):
         """K = len(actions) steps in ONE launch (mgx_rollout_compact): actions int32 [K, N] known up
         front (a random-action or scripted rollout); observations t+1 .. t+K, rewards / dones of
         steps t .. t+K-1 -- the same as K step() calls, bit for bit.  The K steps must lie within one
-        refill epoch of the engine."""
+        refill epoch of the engine.
+        gae: dict(values f32 [K, N], last_values f32 [N], gamma, gae_lambda, out=(adv, ret) f32 [K, N],
+        stats=f64 [3] or None, scratch=None) -- also the GAE of these K steps, fused into the launch
+        (mgx_rollout_compact_gae): gae_dones(rewards[t:t+K], values, dones of the K steps, ...) bit for bit."""
         e = self.engine
         K = int(actions.shape[0])
         if actions.device != e.device or actions.dtype != torch.int32 or tuple(actions.shape) != (K, self.N) \
@@ -108,7 +111,28 @@ class CompactBuffer:
         o.ep_return_dev = e.ep_return.data_ptr()
         o.ep_len_dev = e.ep_len.data_ptr()
         o.livelock_dev = e.livelock.data_ptr()
-        _lib.check(e.L.mgx_rollout_compact(e.h, _ptr(actions), K, ctypes.byref(o), e._stream()), "mgx_rollout_compact")
+        if gae is None:
+            _lib.check(e.L.mgx_rollout_compact(e.h, _ptr(actions), K, ctypes.byref(o), e._stream()),
+                       "mgx_rollout_compact")
+        else:
+            from .engine import _scratch_for
+            v, lv = gae["values"], gae["last_values"].reshape(self.N).float().contiguous()
+            adv, ret = gae["out"]
+            for x in (v, adv, ret):
+                if x.dtype != torch.float32 or tuple(x.shape) != (K, self.N) or not x.is_contiguous() \
+                        or x.device != e.device:
+                    raise ValueError("GAE values / advantages / returns must be contiguous f32 [%d, %d]" % (K, self.N))
+            stats = gae.get("stats")
+            g = _lib.MgxGaeArgs()
+            g.values_dev, g.last_values_dev = v.data_ptr(), lv.data_ptr()
+            g.gamma = float(gae["gamma"])
+            g.gamma_lambda = float(torch.tensor(gae["gamma"] * gae["gae_lambda"], dtype=torch.float64).float())
+            g.advantages_dev, g.returns_dev = adv.data_ptr(), ret.data_ptr()
+            g.adv_stats_dev = stats.data_ptr() if stats is not None else None
+            sc = _scratch_for(stats, gae.get("scratch")) if stats is not None else None
+            g.stats_scratch_dev = sc.data_ptr() if sc is not None else None
+            _lib.check(e.L.mgx_rollout_compact_gae(e.h, _ptr(actions), K, ctypes.byref(o), ctypes.byref(g),
+                                                   e._stream()), "mgx_rollout_compact_gae")
         e.calls += K
 
     def carry_over(self):

@@ -383,14 +383,15 @@ def test_full_size_matches_oracle(problem, mission, size, n, T, layout):
     eng.poll_error()
 
 
-@pytest.mark.parametrize("layout", ["fused", "compact"])
+@pytest.mark.parametrize("layout", ["fused", "fused_gae", "compact"])
 @pytest.mark.parametrize("n", [8192, 65536])
 def test_bench_shape_graph_matches_oracle(n, layout):
     """The exact shape bench.py times -- the driver's `--steps 20` line: GTG 8x8, terminal_mode
     'truncated', refill epoch E = 20 = horizon H, one hipGraph per chunk holding the carry-over, the
     steps, mgx_gae_dones with the adv-stat triple and mgx_join -- replayed 4 times with new actions in
     its static buffer.  `fused` (the headline): ONE mgx_rollout_compact launch of the 20 steps (it
-    forks the epoch's refill); `compact`: 20 mgx_step_compact launches (the per-step line).  Every
+    forks the epoch's refill); `fused_gae`: the same launch with the GAE fused in (mgx_rollout_compact_gae,
+    the bench's graph at E = H); `compact`: 20 mgx_step_compact launches (the per-step line).  Every
     replay: each step's observation rows, mission ids, dones, terminated / truncated flags and f32
     rewards vs the C oracle, the terminal row of every env that was truncated, GAE advantages /
     returns bit-exact vs numpy and the (sum A, sum A^2, n) triple; at the end every env's state."""
@@ -413,7 +414,7 @@ def test_bench_shape_graph_matches_oracle(n, layout):
     ov.reset()
     eng.reset()
     buf.observe(0)
-    fused = layout == "fused"
+    fused = layout in ("fused", "fused_gae")        # fused_gae: the driver's graph, GAE in the rollout launch
     for t in range(0, W, E if fused else 1):
         if t and t % E == 0:
             buf.carry_over()
@@ -438,12 +439,16 @@ def test_bench_shape_graph_matches_oracle(n, layout):
         gr.capture_begin()
         st.zero_()
         buf.carry_over()
-        if fused:
+        if layout == "fused_gae":
+            buf.rollout(0, static, gae=dict(values=vals, last_values=last_v, gamma=gamma, gae_lambda=lam,
+                                            out=(adv, ret), stats=st))
+        elif fused:
             buf.rollout(0, static)
         else:
             for j in range(E):
                 buf.step(j, static[j])
-        gae_dones(buf.rewards, vals, buf.dones, last_v, gamma, lam, stats=st, out=(adv, ret))
+        if layout != "fused_gae":
+            gae_dones(buf.rewards, vals, buf.dones, last_v, gamma, lam, stats=st, out=(adv, ret))
         eng.join()
         gr.capture_end()
     torch.cuda.synchronize()
