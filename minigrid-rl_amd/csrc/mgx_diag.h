@@ -26,7 +26,8 @@
 
 // ---- elimination builds: the outputs are then NOT the reference's -------------------------------
 #ifndef MGX_GEN_SKIP        // skip generator sections: 1 keys + objects, 2 door positions, 4 goal + agent,
-#define MGX_GEN_SKIP 0      // 8 walls + door draws; inside the keys + objects loop 32 the object choice draw
+#define MGX_GEN_SKIP 0      // 8 walls + door draws; inside the keys + objects loop 32 the object choice draw;
+                            // 64 the refill's mission-token copy into the ring header (SB3 layout's tokens)
 #endif
 #ifndef MGX_DIAG_SKIP       // mgx_step_kernel: skip store classes (2 stack roll, 4 missions, 16 grids)
 #define MGX_DIAG_SKIP 0

@@ -1796,8 +1796,10 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
                     dst[c] = make_uint4(q[0], q[1], q[2], q[3]);
                 }
                 p.ring_hdr[3 * slot] = pack_hdr(G, R);
-                p.ring_hdr[3 * slot + 1] = tok0;
-                p.ring_hdr[3 * slot + 2] = tok1;
+                if (!(MGX_GEN_SKIP & 64)) {                // (elimination build 64: no token copy)
+                    p.ring_hdr[3 * slot + 1] = tok0;
+                    p.ring_hdr[3 * slot + 2] = tok1;
+                }
                 rng_snapshot(G, p.ring_rng + 2 * slot);
                 if (EXT && p.has_move) p.ring_range[slot] = R.range;
                 tail++;

@@ -34,6 +34,7 @@ declare -A V=(
   [topup2]="-DMGX_MT_TOPUP=2"
   [r3rounds]="-DMGX_REFILL_ROUNDS=1"
   [nos8r_serial]="-DMGX_REFILL_S8=0 -DMGX_SERIAL_REFILL=1"
+  [notok]="-DMGX_GEN_SKIP=64"
   [wg16_serial]="-DMGX_MT_WG1=16 -DMGX_SERIAL_REFILL=1"
 )
 names=("$@")
