@@ -55,6 +55,9 @@
 #ifndef MGX_ROLL_DEFER_ROWS  // 1: fused rollout copies step t's rows out during step t + 1's logic (waves 1-3)
 #define MGX_ROLL_DEFER_ROWS 1
 #endif
+#ifndef MGX_ROLL_POPCNT      // 1: the rollout counts a step's resets by ballot + popcount (0: an LDS atomic per pop)
+#define MGX_ROLL_POPCNT 1
+#endif
 #ifndef MGX_ROLL_S8         // 1: S = 8 runs the rollout kernel compiled for S = 8 (0: the generic one)
 #define MGX_ROLL_S8 1
 #endif

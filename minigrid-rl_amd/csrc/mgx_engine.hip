@@ -1416,7 +1416,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                         rhead++;
                         s_head[lanev] = rhead;
                         nh = rhead;
-                        atomicAdd(&s_cnt[0], 1ull);
+                        if (!MGX_ROLL_POPCNT) atomicAdd(&s_cnt[0], 1ull);
                         if (h.z) atomicAdd(&s_cnt[1], (unsigned long long)h.z);
                         lvl = (int)h.z;
                     } else {
@@ -1439,7 +1439,13 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 s_popb[lanev] = popb;
                 s_nh[tb][lanev] = nh;
                 const unsigned long long tm = __ballot(tw);
-                if (lanev == 0) s_tmask = tm;
+                // resets: one popcount of the wave's pops, added by lane 0 (only wave 0 writes s_cnt), instead of
+                // a 64-bit LDS atomic per popping lane on one address (MGX_ROLL_POPCNT)
+                const unsigned long long pm = MGX_ROLL_POPCNT ? __ballot(popb != 0xFF) : 0ull;
+                if (lanev == 0) {
+                    s_tmask = tm;
+                    if (MGX_ROLL_POPCNT) s_cnt[0] += (unsigned long long)__popcll(pm);
+                }
             }
             RSTAMP(1);                                     // step logic (wave 0)
             sync_keep_vm<MGX_ROLL_VMKEEP>();

@@ -35,6 +35,7 @@ declare -A V=(
   [r3rounds]="-DMGX_REFILL_ROUNDS=1"
   [nos8r_serial]="-DMGX_REFILL_S8=0 -DMGX_SERIAL_REFILL=1"
   [notok]="-DMGX_GEN_SKIP=64"
+  [popatomic]="-DMGX_ROLL_POPCNT=0"
   [wg16_serial]="-DMGX_MT_WG1=16 -DMGX_SERIAL_REFILL=1"
 )
 names=("$@")
