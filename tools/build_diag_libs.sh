@@ -22,6 +22,8 @@ declare -A V=(
   [epw32]="-DMGX_REFILL_EPW=32"
   [epw16]="-DMGX_REFILL_EPW=16"
   [prio3]="-DMGX_REFILL_PRIO=3"
+  [prio1]="-DMGX_REFILL_PRIO=1"
+  [prio0]="-DMGX_REFILL_PRIO=0"
   [vmsync]="-DMGX_ROLL_VMKEEP=-1"
   [nodefer]="-DMGX_ROLL_DEFER_ROWS=0"
   [vm0]="-DMGX_ROLL_VMKEEP=0"

@@ -7,6 +7,7 @@
 #   EXP=defer   rows copied out a step late (product) vs at the end of the step          (nodefer)
 #   EXP=step8   per-step kernel compiled for S = 8 (product) vs generic                  (nostep8)
 #   EXP=refill  refill priority 3, MT top-ups, token copy                                (prio3, topup2, topup4, notok)
+#   EXP=prio    refill issue priority 2 (product) vs 1 / 0                               (prio1, prio0)
 #   EXP=pop     resets by ballot + popcount (product) vs per-pop LDS atomics              (popatomic)
 #   EXP=gae     the driver's line with the GAE fused into the rollout launch (bench.py --gae-fused 1) vs not
 set -e
@@ -24,6 +25,9 @@ case "${EXP:?set EXP}" in
           TAG=dfc5 ROUNDS=1 LIBS="- $L/libmgx_nodefer.so" BENCH_ARGS="--config 5" bash tools/gpu_ab.sh ;;
   step8)  TAG=st8 ROUNDS=2 LIBS="- $L/libmgx_nostep8.so" BENCH_ARGS="--layout compact --steps 256 --warmup 256" bash tools/gpu_ab.sh ;;
   refill) TAG=rf20 ROUNDS=2 LIBS="- $L/libmgx_prio3.so $L/libmgx_topup2.so $L/libmgx_topup4.so $L/libmgx_notok.so" BENCH_ARGS="$K20" bash tools/gpu_ab.sh ;;
+  prio)   TAG=pr20 ROUNDS=3 LIBS="- $L/libmgx_prio1.so $L/libmgx_prio0.so" BENCH_ARGS="$K20" bash tools/gpu_ab.sh
+          TAG=pr2048 ROUNDS=1 LIBS="- $L/libmgx_prio1.so $L/libmgx_prio0.so" BENCH_ARGS="" bash tools/gpu_ab.sh
+          TAG=prc4 ROUNDS=1 LIBS="- $L/libmgx_prio1.so $L/libmgx_prio0.so" BENCH_ARGS="--config 4" bash tools/gpu_ab.sh ;;
   pop)    TAG=pc2048 ROUNDS=2 LIBS="- $L/libmgx_popatomic.so" BENCH_ARGS="" bash tools/gpu_ab.sh ;;
   gae)    for r in 1 2 3; do for g in 1 0; do
             timeout -k 10 240 python bench.py $K20 --cpu-seconds 0 --both-layouts 0 --gae-fused $g > gpurun_out/gae_line.json 2> gpurun_out/gae_err.log || { tail -20 gpurun_out/gae_err.log; exit 1; }
