@@ -60,9 +60,6 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "env-steps/sec at 65k parallel envs, 1/2/4/8 MI355X; % HBM roofline"
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_STEP = 334                    # per env-step algorithmic bytes
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
-PMC_FILE_COMPACT = os.path.join(ROOT, "profiles", "pmc_step_kernel_compact.json")
-PMC_FILE_FUSED = os.path.join(ROOT, "profiles", "pmc_rollout_kernel.json")
 
 
 def parse():
@@ -377,6 +374,25 @@ def _rocprof_trace_timed_avg(path, kernel, first, count):
     return sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in sel) / 1e3 / count
 
 
+def _profile_dir():
+    """(profiles/<round>_pmc directory whose manifest.json names the libmgx.so this process loaded, its
+    hash): committed rocprof figures are reported only for the build they were collected with."""
+    import glob
+    import hashlib
+    from mgx import _lib
+    try:
+        sha = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None, None
+    for man in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc", "manifest.json")), reverse=True):
+        try:
+            if json.load(open(man)).get("lib_sha16") == sha:
+                return os.path.dirname(man), sha
+        except (OSError, ValueError):
+            continue
+    return None, sha
+
+
 def pick_epoch(K, D=256):
     """Refill epoch E (mgx refill_every) so that the K timed steps are whole epochs: the largest
     divisor of K in [8, min(64, D/4)] (at D/2 the ring invariant 2E <= D makes every epoch refill the
@@ -441,6 +457,9 @@ def measure_rollout(args, layout, world, rank, dev):
     eng = MgxEngine(problem=args.problem, mission=mission, size=args.size, n_envs=n, seed=42,
                     env_index_offset=rank * n, n_stack=args.n_stack, terminal_mode="truncated", device=dev,
                     refill_every=E or 0, refill_cap=args.refill_cap, ring_depth=args.ring_depth)
+    # device kernel clocks (mgx_set_clock): every step-kernel and refill launch records its own span, so the
+    # roofline prices the kernel's launches INSIDE the timed graph replays (set before any capture)
+    eng.enable_clock()
     E = eng.refill_every
     H = pick_horizon(K, E if aligned else None, args.horizon or 0)
     # warm-up: whole refill epochs, and at least --min-warmup (256) steps.  mgx_reset fills every ring
@@ -463,7 +482,10 @@ def measure_rollout(args, layout, world, rank, dev):
         # compact layout: each step writes its observation row, reward and done straight into the
         # rollout buffer (mgx_step_compact); GAE reads the buffer's rewards and dones
         from mgx.compact import CompactBuffer
-        cbuf = CompactBuffer(eng, H)
+        # ring layout: a horizon's history rows are the previous horizon's last rows, read in place -- the
+        # per-horizon carry-over is a block advance, not a copy (every timed horizon pays for what
+        # a steady-state horizon costs, and no copy exists outside the graphs)
+        cbuf = CompactBuffer(eng, H, ring=True)
         rew, dones = cbuf.rewards, cbuf.dones
     else:
         rew = torch.zeros((H, n), dtype=torch.float32, device=dev)
@@ -500,8 +522,7 @@ def measure_rollout(args, layout, world, rank, dev):
 
     def chunk(c):
         if compact:
-            if c:
-                cbuf.carry_over()
+            cbuf.carry_over()                            # every horizon starts a rollout (ring: no copy)
             if fused and E == H and args.gae_fused:      # one launch for the horizon, its GAE fused in
                 cbuf.rollout(0, actions[W + c * H:W + c * H + E], gae=dict(
                     values=vals, last_values=last_v, gamma=gamma, gae_lambda=lam, out=(adv, ret), stats=hist[c],
@@ -516,22 +537,29 @@ def measure_rollout(args, layout, world, rank, dev):
             for j in range(H):
                 eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
         if not (fused and E == H and args.gae_fused):
-            gae_dones(rew, vals, dones, last_v, gamma, lam, stats=hist[c], scratch=scratch, out=(adv, ret))
+            gae_dones(rew, vals, cbuf.dones if compact else dones, last_v, gamma, lam, stats=hist[c], scratch=scratch,
+                      out=(adv, ret))                    # (ring: this horizon's block of start flags)
         eng.join()                                       # the epoch's refill (it ran beside GAE): the
                                                          # chunk's graph is self-contained, and the region
                                                          # pays for every refill it forked
 
     graphs = []
     forks0 = eng.stats()["refill_launches"]
+    # ring buffer: graph c writes block (c0 + c + 1) % m; replayed in cyclic order, the graphs continue the
+    # block sequence only if there is a multiple of m of them (one 20-step chunk -> two graphs, alternating)
+    ng = nchunks
+    if compact and args.graph:
+        m = cbuf.blocks
+        ng = -(-nchunks // m) * m
     if args.graph:
         # one hipGraph per horizon chunk (launch-bound loop -> one replay each); a chunk is whole
         # refill epochs, so each graph holds its forks and joins (self-contained capture)
         s = torch.cuda.Stream(dev)
         with torch.cuda.stream(s):
-            for c in range(nchunks):
+            for c in range(ng):
                 gr = torch.cuda.CUDAGraph()
                 gr.capture_begin()
-                chunk(c)
+                chunk(c % nchunks)
                 gr.capture_end()
                 graphs.append(gr)
         # one untimed replay of each graph (more warm-up steps: every graph is whole refill epochs
@@ -545,6 +573,7 @@ def measure_rollout(args, layout, world, rank, dev):
     # graphs, replayed once each; eagerly, counted as they run)
     forks = (st0["refill_launches"] - forks0) if graphs else None
     hist.zero_()                                         # (the untimed replays accumulated into it)
+    clk0 = (eng.clock_launches(0), eng.clock_launches(1))    # kernel-clock launch counts at the region's start
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -565,6 +594,9 @@ def measure_rollout(args, layout, world, rank, dev):
         dist.barrier()
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+    clk1 = (eng.clock_launches(0), eng.clock_launches(1))
+    timed_step_us = eng.clock_spans_us(0, clk0[0], clk1[0])      # the timed region's own kernel launches
+    timed_refill_us = eng.clock_spans_us(1, clk0[1], clk1[1])
     st1 = eng.stats()
     eng.poll_error()
     # roofline probe: per-launch duration of mgx_step_kernel (HIP events on its stream) in the
@@ -622,13 +654,17 @@ def measure_rollout(args, layout, world, rank, dev):
     probe_us = []
     for a0, a1, cnt in windows:
         probe_us += [a0.elapsed_time(a1) * 1e3 / cnt] * cnt
-    elapsed = torch.tensor([wall, gpu_ms / 1e3], dtype=torch.float64, device=dev)
+    per = E if fused else 1                              # steps per step-kernel launch
+    step_us = sum(timed_step_us) / len(timed_step_us) / per if timed_step_us else float("nan")
+    refill_us = sum(timed_refill_us) / len(timed_refill_us) if timed_refill_us else float("nan")
+    elapsed = torch.tensor([wall, gpu_ms / 1e3, step_us, refill_us], dtype=torch.float64, device=dev)
     steps_done = torch.tensor([float(st1["steps"] - st0["steps"]), float(st1["resets"] - st0["resets"])],
                               dtype=torch.float64, device=dev)
     if world > 1:
         elapsed = _allreduce(elapsed, dist.ReduceOp.MAX)
         steps_done = _allreduce(steps_done, dist.ReduceOp.SUM)
     wall_max, gpu_max = float(elapsed[0]), float(elapsed[1])
+    step_us_max, refill_us_max = float(elapsed[2]), float(elapsed[3])
     total_env_steps, total_resets = float(steps_done[0]), float(steps_done[1])
     assert int(total_env_steps) == n * K * world, (total_env_steps, n * K * world)
     hs = hist.cpu().numpy()
@@ -636,45 +672,57 @@ def measure_rollout(args, layout, world, rank, dev):
     gae_h = gae_probe(dev, n, H)
     gae_1k = gae_probe(dev, n, 1024) if H != 1024 else gae_h
     if rank == 0:
-        per_launch_s = (sum(probe_us) / len(probe_us)) * 1e-6 if probe_us else float(gpu_ms) / 1e3 / K
+        probe_s = (sum(probe_us) / len(probe_us)) * 1e-6 if probe_us else None
         resets_per_launch = (st1["resets"] - st0["resets"]) / K
         b_alg = B_STEP * n + (3 * args.size ** 2 + 208) * resets_per_launch
+        # THE roofline duration: the kernel's own launches inside the timed region, per step, from the device
+        # clock (first workgroup start -> last workgroup end of each launch; the max over ranks)
+        per_launch_s = step_us_max * 1e-6
         achieved = b_alg / per_launch_s / 1e9
+        prof_dir, lib_sha = _profile_dir()
         traffic, traffic_src = None, None
-        # rocprofv3 PMC HBM bytes of this kernel at this config AND launch shape (a fused launch of E steps
-        # moves per step what E steps share: the PMC file must have steps_per_launch == E), committed under
-        # profiles/r04_pmc/ (tools/gpu_r4_profiles.sh), else an older round's matching file
-        import glob
-        spl = E if fused else 1
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04_pmc", "pmc_[0-9]_%s*.json" % layout)))
-        cands += sorted(glob.glob(os.path.join(ROOT, "profiles", "r03_pmc", "pmc_[0-9]_%s.json" % layout)))
-        cands += [PMC_FILE_FUSED if fused else (PMC_FILE_COMPACT if compact else PMC_FILE)]
-        for pmc_file in cands:
-            try:
-                pmc = json.load(open(pmc_file))
-            except (OSError, ValueError):
-                continue
-            if (pmc.get("n_envs") == n and pmc.get("size") == args.size and pmc.get("mission") == mission
-                    and pmc.get("steps_per_launch", 1) == spl):
-                traffic = pmc.get("hbm_bytes_per_launch")
-                if traffic is not None:                  # per step (a fused launch holds several)
-                    traffic = traffic / spl
-                    traffic_src = os.path.relpath(pmc_file, ROOT)
-                break
-        # the same kernel's average duration from the committed rocprofv3 kernel stats of this exact command
-        # shape (profiles/r04_pmc/kernel_stats_<cfg>_<layout>_e<E>.csv): `frac` recomputed from profiles/
-        kstat = _rocprof_kernel_avg(os.path.join(ROOT, "profiles", "r04_pmc", "kernel_stats_%d_%s_e%d.csv" % (
-            args.config, layout, spl if fused else E)), "mgx_rollout_kernel" if fused else
-            ("mgx_step_kernel<int, true" if compact else "mgx_step_kernel<int, false"))   # (<..., 8>: the S = 8 instance)
-        # ... and over the timed region's launches alone, from the committed kernel trace of the same command:
-        # in the timed graph replays the epoch's refill is dispatched ahead of the rollout and the kernel runs
-        # longer than in the eager probe windows above
+        spl = per
+        if prof_dir is not None:
+            # rocprofv3 PMC HBM bytes of this kernel at this config AND launch shape (a fused launch of E steps
+            # moves per step what E steps share: the PMC file must have steps_per_launch == E), committed under
+            # profiles/<round>_pmc/ for THIS build (manifest.json: the libmgx.so hash it was collected with)
+            import glob
+            for pmc_file in sorted(glob.glob(os.path.join(prof_dir, "pmc_[0-9]_%s*.json" % layout))):
+                try:
+                    pmc = json.load(open(pmc_file))
+                except (OSError, ValueError):
+                    continue
+                if (pmc.get("n_envs") == n and pmc.get("size") == args.size and pmc.get("mission") == mission
+                        and pmc.get("steps_per_launch", 1) == spl):
+                    traffic = pmc.get("hbm_bytes_per_launch")
+                    if traffic is not None:              # per step (a fused launch holds several)
+                        traffic = traffic / spl
+                        traffic_src = os.path.relpath(pmc_file, ROOT)
+                    break
         kname = "mgx_rollout_kernel" if fused else ("mgx_step_kernel<int, true" if compact else "mgx_step_kernel<int, false")
-        per = E if fused else 1                                  # steps per launch
-        t_avg = _rocprof_trace_timed_avg(os.path.join(ROOT, "profiles", "r04_pmc", "kernel_trace_%d_%s_e%d.csv.gz" % (
-            args.config, layout, spl if fused else E)), kname, (W + (K if graphs else 0)) // per, K // per)
-        if kstat is not None and t_avg is not None:
-            kstat["timed_avg_us"] = t_avg
+        kstat = None
+        if prof_dir is not None:
+            # the same kernel's average duration from the committed rocprofv3 kernel stats of this exact command
+            # shape (kernel_stats_<cfg>_<layout>_e<E>.csv), and over the timed region's launches alone from the
+            # committed kernel trace of the same command (kernel_trace_*.csv.gz): the cross-check of the device clock
+            kstat = _rocprof_kernel_avg(os.path.join(prof_dir, "kernel_stats_%d_%s_e%d.csv" % (
+                args.config, layout, spl if fused else E)), kname)
+            t_avg = _rocprof_trace_timed_avg(os.path.join(prof_dir, "kernel_trace_%d_%s_e%d.csv.gz" % (
+                args.config, layout, spl if fused else E)), kname, (W + (ng * H if graphs else 0)) // per, K // per)
+            if kstat is not None and t_avg is not None:
+                kstat["timed_avg_us"] = t_avg
+        produced = (st1["resets"] - st0["resets"]) + (st1["queued"] - st0["queued"])
+        consumed = st1["resets"] - st0["resets"]
+        refill_launches = forks if forks is not None else st1["refill_launches"] - st0["refill_launches"]
+        # the refill (episode generator) inside the timed region: SURVEY §8(d) 400 B per episode produced
+        refill = None
+        if timed_refill_us:
+            b_ref = 400.0 * produced / max(refill_launches, 1)
+            refill = {"launches": len(timed_refill_us), "avg_launch_us": refill_us_max,
+                      "steps_per_launch": E, "episodes_per_launch": produced / max(refill_launches, 1),
+                      "alg_bytes_per_launch": b_ref, "achieved": b_ref / refill_us_max / 1e3,
+                      "frac": b_ref / refill_us_max / 1e3 / PEAK_HBM_GBPS, "unit": "GB/s",
+                      "note": "mgx_refill kernel launches of the timed region (device clock, beside the rollout)"}
         # VecFrameStack image + direction roll (reported separately); the compact layout rolls nothing
         stack_bytes = 0 if compact else n * (441 + 588 + 12 + 16)
         out = {
@@ -708,10 +756,14 @@ def measure_rollout(args, layout, world, rank, dev):
                            "all-reduce (%s)" % dist.get_backend() if world > 1 else "accumulation", H,
                            " (fused into the rollout launch: mgx_rollout_compact_gae)" if fused and E == H and args.gae_fused
                            else "")},
-            "window": {"refill_launches": forks if forks is not None else st1["refill_launches"] - st0["refill_launches"],
-                       "episodes_produced": (st1["resets"] - st0["resets"]) + (st1["queued"] - st0["queued"]),
-                       "episodes_consumed": st1["resets"] - st0["resets"],
-                       "gae_launches": nchunks},
+            # every episode the timed steps consumed is paid for by a refill inside the region; when the region
+            # (one 20-step refill epoch on the driver's line) produced fewer than it consumed, value_resets_paid
+            # prices the shortfall in at the region's own production rate
+            "value_resets_paid": total_env_steps / wall_max * min(1.0, produced / max(consumed, 1)),
+            "window": {"refill_launches": refill_launches, "episodes_produced": produced,
+                       "episodes_consumed": consumed, "produced_over_consumed": produced / max(consumed, 1),
+                       "gae_launches": nchunks, "graphs": len(graphs),
+                       "carry_over": "ring rows (no copy)" if compact else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": ("mgx_rollout_kernel<false> (fused: %d steps per launch; per-step figures = "
@@ -719,17 +771,27 @@ def measure_rollout(args, layout, world, rank, dev):
                                     "mgx_step_kernel<int, true[, 8]> (compact)" if compact else
                                     "mgx_step_kernel<int, false[, 8]> (SB3 stacks)"),
                          "avg_launch_us": per_launch_s * 1e6,
+                         "timing": "device clock (mgx_set_clock): the kernel's %d launches inside the timed region, "
+                                   "first workgroup start to last workgroup end, per step; max over ranks"
+                                   % len(timed_step_us),
+                         "timed_launches": len(timed_step_us),
+                         "probe_avg_launch_us": probe_s * 1e6 if probe_s else None,
+                         "probe_frac": (b_alg / probe_s / 1e9 / PEAK_HBM_GBPS) if probe_s else None,
+                         "probe_note": "HIP events around eager probe launches after the region (rollout dispatched "
+                                       "first, previous refill joined): not the timed region's regime",
+                         "refill": refill,
+                         "build": lib_sha,
                          "rocprof": None if kstat is None else {
                              "source": kstat["source"], "avg_launch_us": kstat["avg_us"] / spl,
                              "frac": b_alg / (kstat["avg_us"] / spl * 1e-6) / 1e9 / PEAK_HBM_GBPS,
                              "note": "the committed rocprofv3 --stats average of the same kernel at this config and "
-                                     "launch shape (per step; all its launches: warm-up, graph replays, probe), "
-                                     "B_alg of this run",
+                                     "launch shape, collected with this build (per step; all its launches: warm-up, "
+                                     "graph replays, probe), B_alg of this run",
                              "timed_avg_us": (kstat["timed_avg_us"] / spl) if "timed_avg_us" in kstat else None,
                              "timed_frac": (b_alg / (kstat["timed_avg_us"] / spl * 1e-6) / 1e9 / PEAK_HBM_GBPS)
                              if "timed_avg_us" in kstat else None,
                              "timed_note": "the timed region's launches alone (committed kernel trace of the same "
-                                           "command, per step): the graph replays, refill dispatched first"},
+                                           "command, per step)"},
                          "probe_launches": len(probe_us),
                          "step_pipeline_us": float(gpu_ms) * 1e3 / K,
                          "alg_bytes_per_launch": b_alg, "resets_per_launch": resets_per_launch,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MGX_ABI_VERSION 5
+#define MGX_ABI_VERSION 6
 
 /* Live-lock cap (engine policy; the reference hangs): a
  * reset attempt may consume at most this many MT19937 words; the attempt that
@@ -230,6 +230,15 @@ mgx_status mgx_gather(const mgx_handle *h, const uint8_t *rows_dev, const uint8_
                       const uint8_t *terminal_rows_dev, void *image_dev, int image_f32, void *direction_dev,
                       int direction_f32, uint8_t *mission_dev, void *stream);
 
+/* mgx_gather over a RING of ring_rows rows (ABI 6): walking back from a sample's newest row wraps
+ * from row 0 to row ring_rows - 1, so a rollout that starts where the previous one ended reads its
+ * n_stack - 1 history rows in place -- no per-rollout copy of them (mgx/compact.py ring mode).
+ * ring_rows = 0 is mgx_gather; else ring_rows >= n_stack. */
+mgx_status mgx_gather_ring(const mgx_handle *h, const uint8_t *rows_dev, const uint8_t *mission_ids_dev,
+                           const uint8_t *starts_dev, int64_t n_envs, int64_t ring_rows, const int64_t *index_dev,
+                           int64_t n_samples, const uint8_t *terminal_rows_dev, void *image_dev, int image_f32,
+                           void *direction_dev, int direction_f32, uint8_t *mission_dev, void *stream);
+
 /* Makes `stream` wait for the in-flight refill, if any (no host sync). */
 mgx_status mgx_join(mgx_handle *h, void *stream);
 
@@ -288,6 +297,19 @@ mgx_status mgx_rollout_compact_gae(mgx_handle *h, const int32_t *actions_dev, in
  * Synchronises `stream`. */
 #define MGX_SCENE_WORDS 104
 mgx_status mgx_scene(mgx_handle *h, int64_t env, uint32_t *record, void *stream);
+
+/* Kernel clocks (measurement; ABI 6).  With clock_dev set, every launch of the step kernels
+ * (mgx_step, mgx_step_compact, mgx_rollout_compact[_gae]: class 0) and of the refill kernel (class 1)
+ * records on the device the span from its first workgroup's start to its last workgroup's end, so
+ * that a caller can time the kernels INSIDE a replayed hipGraph, beside whatever runs concurrently
+ * (bench.py: the timed region's own launches).  clock_dev: u64 [MGX_CLOCK_CLASSES][MGX_CLOCK_HDR +
+ * 2 * slots], caller-owned, zeroed.  Per class: [0] launches so far, [1] internal, then for launch
+ * i < slots: [MGX_CLOCK_HDR + 2i] = ~start, [MGX_CLOCK_HDR + 2i + 1] = end (wall-clock ticks;
+ * *tick_khz, optional, receives their rate).  Kernel parameters are captured at launch: set the clock
+ * before capturing a graph.  NULL clock_dev: off (the default). */
+#define MGX_CLOCK_CLASSES 2
+#define MGX_CLOCK_HDR 4
+mgx_status mgx_set_clock(mgx_handle *h, uint64_t *clock_dev, int slots, int *tick_khz);
 
 /* Synchronises `stream`, returns the device error bits (MGX_DEVERR_*) and clears them. */
 mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits);

@@ -144,7 +144,39 @@ struct KParams {
                             // 1 the wave's mean deficit (<= cap), 2 its mean consumption, rounded up
     uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
                             //        generation (mgx_scene regenerates it), else null
+    unsigned long long *clk;  // mgx_set_clock: per kernel class [CLK_HDR + 2 * clk_slots] launch spans, or null
+    int clk_slots;
 };
+
+// ---- kernel clocks (mgx_set_clock; include/mgx.h).  Each launch of a clocked kernel records the span from its
+// first workgroup's start to its last workgroup's end in wall-clock ticks (s_memrealtime), so that a caller can
+// time a kernel INSIDE a replayed hipGraph, beside whatever runs concurrently (bench.py's roofline: the timed
+// region's own launches, not an eager probe).  Class block: [0] launches so far, [1] workgroups of the running
+// launch that have finished, [2..3] unused, then per launch i < slots: [CLK_HDR + 2i] = ~(first start) (a max
+// of complements, so that a zeroed block works), [CLK_HDR + 2i + 1] = last end.  One thread per workgroup; the
+// launch's last workgroup (fenced counter) advances [0] -- every workgroup read it before that.
+constexpr int CLK_HDR = 4;
+enum { CLK_STEP = 0, CLK_REFILL = 1, CLK_CLASSES = 2 };
+__device__ __forceinline__ unsigned long long *clk_block(const KParams &p, int cls) {
+    return p.clk + (size_t)cls * (size_t)(CLK_HDR + 2 * p.clk_slots);
+}
+__device__ __forceinline__ void clk_begin(const KParams &p, int cls) {   // one thread per workgroup
+    unsigned long long *c = clk_block(p, cls);
+    const unsigned long long t = (unsigned long long)wall_clock64();
+    const unsigned long long seq = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seq < (unsigned long long)p.clk_slots) atomicMax(&c[CLK_HDR + 2 * seq], ~t);
+}
+__device__ __forceinline__ void clk_end(const KParams &p, int cls) {     // one thread per workgroup, at its end
+    unsigned long long *c = clk_block(p, cls);
+    const unsigned long long t = (unsigned long long)wall_clock64();
+    const unsigned long long seq = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seq < (unsigned long long)p.clk_slots) atomicMax(&c[CLK_HDR + 2 * seq + 1], t);
+    __threadfence();
+    if (atomicAdd(&c[1], 1ull) == (unsigned long long)gridDim.x - 1ull) {   // the launch's last workgroup
+        atomicExch(&c[1], 0ull);
+        atomicExch(&c[0], seq + 1ull);
+    }
+}
 
 struct KOut {
     uint8_t *img, *dir;
@@ -654,6 +686,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     const int ne = (int)min<int64_t>(BLOCK_ENVS, p.n - e0);
     const int S = SC > 0 ? SC : p.S;
     if (tid == 0) s_ll = 0;
+    if (p.clk && tid == 0) clk_begin(p, CLK_STEP);
     // issue priority over the refill's waves on the same SIMD (MGX_STEP_PRIO; wave-uniform)
     if (p.step_prio == 1) __builtin_amdgcn_s_setprio(1);
     else if (p.step_prio == 2) __builtin_amdgcn_s_setprio(2);
@@ -1155,6 +1188,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
 #endif
 #endif
     }
+    if (p.clk) {                                  // every wave of the workgroup is done
+        __syncthreads();
+        if (tid == 0) clk_end(p, CLK_STEP);
+    }
 }
 
 // ======================================================= fused rollout kernel
@@ -1239,6 +1276,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     const int S = SC > 0 ? SC : p.S, D = p.D;
     const bool wave0 = tid < BLOCK_ENVS, dmaw = tid >= BLOCK_THREADS;
     const int lc = min(lane, ne - 1);
+    if (p.clk && tid == 0) clk_begin(p, CLK_STEP);
     // ---- setup: ring positions and state (waves 0 and 4), grids (waves 0-3, LDS-DMA)
     if (wave0) {
         s_st[lane] = reinterpret_cast<const uint4 *>(p.state)[e0 + lc];
@@ -1284,12 +1322,13 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         // beside this launch may raise it meanwhile; every value it takes is a completed refill's), shared
         // with the step wave through s_pub so that the staging and the pops agree
         // Visibility of the slots below the value read: every value ring_pubn takes is the tail of a refill
-        // that has COMPLETED (the slide that writes it follows the refill on the refill stream), and a kernel's
-        // stores are released at its end.  The agent-scope load bypasses this CU's L1; the slot lines
-        // themselves are read by this env's workgroup alone (env-contiguous rings), after this load and
-        // after the launch's own L1 invalidate, so no line of them can be stale here.
+        // that has COMPLETED (the slide that writes it follows the refill on the refill stream, and a kernel's
+        // stores are released at its end).  The load is an agent-scope ACQUIRE (ADVICE r3 / VERDICT r4): it
+        // pairs with that release, and the cache invalidate it implies orders every later load of the slots
+        // (LDS-DMA included) after it, whatever the slot lines' history in this CU's caches.  Once per env per
+        // launch.
         const rpos_t rhead = p.ring_head[e0 + lane];
-        const rpos_t rpub = __hip_atomic_load(p.ring_pubn + e0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const rpos_t rpub = __hip_atomic_load(p.ring_pubn + e0 + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         head0 = rhead;
         s_pub[lane] = rpub;
         const int q = (rpos_t)(rpub - rhead);
@@ -1604,6 +1643,10 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         if (s_cnt[1]) atomicAdd(&p.blk[blockIdx.x].z, s_cnt[1]);
         if (s_err) atomicOr(p.err, s_err);
     }
+    if (p.clk) {                                  // every wave of the workgroup is done
+        __syncthreads();
+        if (tid == 0) clk_end(p, CLK_STEP);
+    }
 }
 
 // ============================================================== fixup kernel
@@ -1694,6 +1737,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     if (p.refill_prio == 1) __builtin_amdgcn_s_setprio(1);
     else if (p.refill_prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (p.refill_prio == 3) __builtin_amdgcn_s_setprio(3);
+    if (p.clk && tid == 0) clk_begin(p, CLK_REFILL);
 #if MGX_REFILL_CLOCK
     const unsigned long long rc0 = __builtin_amdgcn_s_memtime();   // diagnostics: wave clocks per launch
     int rc_iters = 0;
@@ -1843,6 +1887,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         b.x = (unsigned long long)csum;
         p.blk[2 * p.nblk + blockIdx.x] = b;
         if (err) atomicOr(p.err, err);
+        if (p.clk) clk_end(p, CLK_REFILL);        // (one wave per workgroup)
     }
 }
 
@@ -2262,7 +2307,7 @@ constexpr int GATHER_TILE = 16;
 constexpr int GATHER_MAXK = 8;
 template <int K, bool F32>   // n_stack and output type are compile-time: every index split is a constant division
 __global__ __launch_bounds__(256) void mgx_gather_kernel(const uint8_t *__restrict__ rows, const uint8_t *__restrict__ mids,
-                                                         const uint8_t *__restrict__ starts, int64_t N,
+                                                         const uint8_t *__restrict__ starts, int64_t N, int64_t R,
                                                          const int64_t *__restrict__ index, int64_t B,
                                                          const uint8_t *__restrict__ newest,
                                                          const uint8_t *__restrict__ mtok, void *__restrict__ img_out,
@@ -2279,7 +2324,14 @@ __global__ __launch_bounds__(256) void mgx_gather_kernel(const uint8_t *__restri
     if (tid < npair) {
         const int bi = tid / K, k = tid - bi * K;                        // k = slot (K-1 = newest)
         const int64_t idx = index[b0 + bi];
-        const int64_t env = idx % N;
+        const int64_t row0 = idx / N, env = idx - row0 * N;
+        // flat index of the row j steps before the newest: linear buffer (R = 0), or a ring of R rows
+        // (mgx_gather_ring: the rows wrap, so a rollout's history rows need no copy)
+        const auto back_idx = [&](int j) -> int64_t {
+            int64_t r = row0 - j;
+            if (R > 0 && r < 0) r += ((-r + R - 1) / R) * R;
+            return r * N + env;
+        };
         const int back = K - 1 - k;                                      // steps back from the newest
         const uint8_t *src = nullptr;
         int mid = -1;
@@ -2289,13 +2341,13 @@ __global__ __launch_bounds__(256) void mgx_gather_kernel(const uint8_t *__restri
             if (back == 0) { src = newest + env * FROW; mid = mids[idx]; }
             else {
                 bool ok = true;
-                for (int j = 0; j < back - 1 && ok; j++) ok = !starts[idx - (int64_t)j * N];
-                if (ok) { const int64_t r = idx - (int64_t)(back - 1) * N; src = rows + r * FROW; mid = mids[r]; }
+                for (int j = 0; j < back - 1 && ok; j++) ok = !starts[back_idx(j)];
+                if (ok) { const int64_t r = back_idx(back - 1); src = rows + r * FROW; mid = mids[r]; }
             }
         } else {
             bool ok = true;
-            for (int j = 0; j < back && ok; j++) ok = !starts[idx - (int64_t)j * N];
-            if (ok) { const int64_t r = idx - (int64_t)back * N; src = rows + r * FROW; mid = mids[r]; }
+            for (int j = 0; j < back && ok; j++) ok = !starts[back_idx(j)];
+            if (ok) { const int64_t r = back_idx(back); src = rows + r * FROW; mid = mids[r]; }
         }
         s_src[tid] = src;
         s_mid[tid] = mid;
@@ -3023,6 +3075,19 @@ mgx_status mgx_set_seed(mgx_handle *h, int64_t seed) {
     return MGX_OK;
 }
 
+mgx_status mgx_set_clock(mgx_handle *h, uint64_t *clock_dev, int slots, int *tick_khz) {
+    if (!h || (clock_dev && slots < 1)) return fail(MGX_ERR_INVALID, "mgx_set_clock: bad argument");
+    static_assert(CLK_CLASSES == MGX_CLOCK_CLASSES && CLK_HDR == MGX_CLOCK_HDR, "include/mgx.h clock layout");
+    h->kp.clk = reinterpret_cast<unsigned long long *>(clock_dev);
+    h->kp.clk_slots = clock_dev ? slots : 0;
+    if (tick_khz) {
+        int khz = 0;
+        HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
+        *tick_khz = khz;
+    }
+    return MGX_OK;
+}
+
 mgx_status mgx_get_config(const mgx_handle *h, mgx_config *out) {
     if (!h || !out) return fail(MGX_ERR_INVALID, "null argument");
     *out = h->cfg;
@@ -3221,9 +3286,19 @@ mgx_status mgx_gather(const mgx_handle *h, const uint8_t *rows_dev, const uint8_
                       const uint8_t *starts_dev, int64_t n_envs, const int64_t *index_dev, int64_t n_samples,
                       const uint8_t *terminal_rows_dev, void *image_dev, int image_f32, void *direction_dev,
                       int direction_f32, uint8_t *mission_dev, void *stream) {
+    return mgx_gather_ring(h, rows_dev, mission_ids_dev, starts_dev, n_envs, 0, index_dev, n_samples,
+                           terminal_rows_dev, image_dev, image_f32, direction_dev, direction_f32, mission_dev, stream);
+}
+
+mgx_status mgx_gather_ring(const mgx_handle *h, const uint8_t *rows_dev, const uint8_t *mission_ids_dev,
+                           const uint8_t *starts_dev, int64_t n_envs, int64_t ring_rows, const int64_t *index_dev,
+                           int64_t n_samples, const uint8_t *terminal_rows_dev, void *image_dev, int image_f32,
+                           void *direction_dev, int direction_f32, uint8_t *mission_dev, void *stream) {
     if (!h || !rows_dev || !mission_ids_dev || !starts_dev || !index_dev || !image_dev || !direction_dev ||
-        !mission_dev || n_envs <= 0 || n_samples < 0)
+        !mission_dev || n_envs <= 0 || n_samples < 0 || ring_rows < 0)
         return fail(MGX_ERR_INVALID, "mgx_gather: bad argument");
+    if (ring_rows > 0 && ring_rows < h->kp.n_stack)
+        return fail(MGX_ERR_INVALID, "mgx_gather_ring: the ring must hold n_stack rows");
     const int K = h->kp.n_stack;
     if (K > GATHER_MAXK) return fail(MGX_ERR_INVALID, "mgx_gather: n_stack > 8");
     if (n_samples == 0) return MGX_OK;
@@ -3233,11 +3308,11 @@ mgx_status mgx_gather(const mgx_handle *h, const uint8_t *rows_dev, const uint8_
     case KK:                                                                                                     \
         if (image_f32)                                                                                           \
             hipLaunchKernelGGL((mgx_gather_kernel<KK, true>), dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, \
-                               rows_dev, mission_ids_dev, starts_dev, n_envs, index_dev, n_samples, terminal_rows_dev, \
+                               rows_dev, mission_ids_dev, starts_dev, n_envs, ring_rows, index_dev, n_samples, terminal_rows_dev, \
                                h->kp.mtok, image_dev, direction_dev, mission_dev);                              \
         else                                                                                                     \
             hipLaunchKernelGGL((mgx_gather_kernel<KK, false>), dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, \
-                               rows_dev, mission_ids_dev, starts_dev, n_envs, index_dev, n_samples, terminal_rows_dev, \
+                               rows_dev, mission_ids_dev, starts_dev, n_envs, ring_rows, index_dev, n_samples, terminal_rows_dev, \
                                h->kp.mtok, image_dev, direction_dev, mission_dev);                              \
         break;
     switch (K) {

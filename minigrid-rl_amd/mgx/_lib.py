@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("MGX_LIB_PATH", os.path.join(HERE, "libmgx.so"))   # o
 
 MGX_OK = 0
 GAE_SCRATCH_WORDS = 512  # == MGX_GAE_SCRATCH_WORDS (include/mgx.h)
-ABI_VERSION = 5        # == MGX_ABI_VERSION (include/mgx.h)
+ABI_VERSION = 6        # == MGX_ABI_VERSION (include/mgx.h)
 PROBLEMS = {"multi": 0, "full": 1, "gto": 2, "gtg": 3, "opn": 4, "pkp": 5, "drp": 6, "mov": 7}
 TERMINAL = {"none": 0, "truncated": 1, "all": 2}
 DEVERR = {1: "MT19937 ring: a cursor left the window of the stream the device holds", 2: "action outside 0..6 (ValueError: Unknown action)",
@@ -26,7 +26,8 @@ DEVERR = {1: "MT19937 ring: a cursor left the window of the stream the device ho
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
            "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_gae_dones", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text",
            "mgx_step_compact", "mgx_rollout_compact", "mgx_rollout_compact_gae", "mgx_observe_compact", "mgx_gather",
-           "mgx_scene")
+           "mgx_gather_ring", "mgx_scene", "mgx_set_clock")
+CLOCK_CLASSES, CLOCK_HDR = 2, 4   # == MGX_CLOCK_CLASSES, MGX_CLOCK_HDR (include/mgx.h)
 
 
 class MgxConfig(ctypes.Structure):
@@ -120,6 +121,8 @@ def load():
     L.mgx_rollout_compact.argtypes = [P, P, I, ctypes.POINTER(MgxRolloutOut), P]
     L.mgx_rollout_compact_gae.argtypes = [P, P, I, ctypes.POINTER(MgxRolloutOut), ctypes.POINTER(MgxGaeArgs), P]
     L.mgx_gather.argtypes = [P, P, P, P, I64, P, I64, P, P, I, P, I, P, P]
+    L.mgx_gather_ring.argtypes = [P, P, P, P, I64, I64, P, I64, P, P, I, P, I, P, P]
+    L.mgx_set_clock.argtypes = [P, P, I, ctypes.POINTER(I)]
     L.mgx_scene.argtypes = [P, I64, ctypes.POINTER(ctypes.c_uint32), P]
     for name in EXPORTS:
         getattr(L, name).restype = getattr(L, name).restype or I

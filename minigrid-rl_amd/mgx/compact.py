@@ -11,7 +11,15 @@ rows (the previous rollout's last observations):
     row H + t   observation t (t = 0..T; row H + T is the observation after the last step)
     starts[r]   1 if row r is an episode's first observation (= `done` of the step before)
 
-so GAE's per-step dones are starts[H+1 : H+T+1] (mgx_gae_dones)."""
+so GAE's per-step dones are starts[H+1 : H+T+1] (mgx_gae_dones).  carry_over() copies the last H + 1
+rows to the front for the next rollout.
+
+ring=True (the bench's and the collector's layout, round 5): the buffer is a ring of m blocks of T rows
+(m = 1 + ceil((H + 1) / T)); rollout c writes its observations 1..T into block c mod m, and its observation
+0 and history rows are the previous rollouts' last rows, read in place (mgx_gather_ring wraps the walk
+back) -- carry_over() only advances the block, no rows move:
+
+    row(t) = (b*T + t - 1) mod R,  b = c mod m,  R = m*T;  dones = starts[b*T : b*T + T]"""
 import ctypes
 
 import torch
@@ -25,11 +33,19 @@ ROW = 148
 class CompactBuffer:
     """Device rollout storage for T steps of an MgxEngine's N envs in the compact layout."""
 
-    def __init__(self, engine, T, device=None):
+    def __init__(self, engine, T, device=None, ring=False):
         self.engine = engine
         self.T, self.N, self.K = int(T), engine.n, engine.n_stack
         self.H = self.K - 1
-        R = self.T + self.H + 1
+        self.ring = bool(ring)
+        self.c = 0                                            # rollouts started (ring: block c % m)
+        if self.ring:
+            self.blocks = 1 + -(-(self.H + 1) // self.T)
+            R = self.blocks * self.T
+        else:
+            self.blocks = 0
+            R = self.T + self.H + 1
+        self.R = R
         dev = device or engine.device
         u8 = dict(dtype=torch.uint8, device=dev)
         self.rows = torch.zeros((R, self.N, ROW), **u8)
@@ -44,12 +60,25 @@ class CompactBuffer:
         self._arange = torch.arange(self.N, device=dev, dtype=torch.int64)
 
     def row(self, t):
-        """Buffer row of observation t."""
+        """Buffer row of observation t (an int or an integer tensor) of the current rollout."""
+        if self.ring:
+            return (self.block * self.T + t - 1) % self.R
         return self.H + t
+
+    @property
+    def block(self):
+        return self.c % self.blocks if self.ring else 0
+
+    def index(self, t, env):
+        """Flat gather index (row * N + env) of observation t of `env`."""
+        return self.row(t) * self.N + env
 
     @property
     def dones(self):
         """u8 [T, N]: done of step t (= start flag of observation t+1)."""
+        if self.ring:
+            b = self.block * self.T
+            return self.starts[b:b + self.T]
         return self.starts[self.H + 1:self.H + 1 + self.T]
 
     def observe(self, t=0):
@@ -122,7 +151,11 @@ class CompactBuffer:
                 if x.dtype != torch.float32 or tuple(x.shape) != (K, self.N) or not x.is_contiguous() \
                         or x.device != e.device:
                     raise ValueError("GAE values / advantages / returns must be contiguous f32 [%d, %d]" % (K, self.N))
+            if lv.device != e.device:
+                raise ValueError("GAE last_values must be on %s" % e.device)
             stats = gae.get("stats")
+            from .engine import _check_stats
+            _check_stats(stats, e.device)
             g = _lib.MgxGaeArgs()
             g.values_dev, g.last_values_dev = v.data_ptr(), lv.data_ptr()
             g.gamma = float(gae["gamma"])
@@ -136,13 +169,17 @@ class CompactBuffer:
         e.calls += K
 
     def carry_over(self):
-        """Start the next rollout: its history rows and observation 0 are this one's last rows."""
+        """Start the next rollout: its history rows and observation 0 are this one's last rows (ring: read in
+        place, only the block advances)."""
+        self.c += 1
+        if self.ring:
+            return
         src = slice(self.T, self.T + self.H + 1)
         for a in (self.rows, self.mids, self.starts):
             a[:self.H + 1].copy_(a[src].clone() if self.T < self.H + 1 else a[src])
 
     def gather(self, index, terminal=False, f32=True, out=None):
-        """Stacked observations of flat buffer indices `index` (i64 [B] = row * N + env):
+        """Stacked observations of flat buffer indices `index` (i64 [B] = row * N + env, see index()):
         dict(image [B, 3K, 7, 7], direction [B, 4K] (f32 = policy input, else u8), mission u8 [B, 32K]).
         terminal=True: the stacked terminal_observation of the step that left row index."""
         e = self.engine
@@ -154,7 +191,8 @@ class CompactBuffer:
                        direction=torch.empty((B, 4 * K), dtype=ft, device=e.device),
                        mission=torch.empty((B, 32 * K), dtype=torch.uint8, device=e.device))
         idx = index.to(torch.int64).contiguous()
-        _lib.check(e.L.mgx_gather(e.h, _ptr(self.rows), _ptr(self.mids), _ptr(self.starts), self.N, _ptr(idx), B,
+        _lib.check(e.L.mgx_gather_ring(e.h, _ptr(self.rows), _ptr(self.mids), _ptr(self.starts), self.N,
+                                       self.R if self.ring else 0, _ptr(idx), B,
                                   _ptr(self.terminal_rows) if terminal else None,
                                   _ptr(out["image"]), int(out["image"].dtype == torch.float32),
                                   _ptr(out["direction"]), int(out["direction"].dtype == torch.float32),
@@ -164,4 +202,4 @@ class CompactBuffer:
     def gather_step(self, t, terminal=False, f32=True, out=None, envs=None):
         """Stacked observation t of every env (or of `envs`)."""
         ix = self._arange if envs is None else envs.to(torch.int64)
-        return self.gather(self.row(t) * self.N + ix, terminal=terminal, f32=f32, out=out)
+        return self.gather(self.index(t, ix), terminal=terminal, f32=f32, out=out)

@@ -157,6 +157,35 @@ class MgxEngine:
         c = self.calls if call is None else call
         return self.ring_depth > 0 and c % self.refill_every == 0
 
+    def enable_clock(self, slots=16384):
+        """Device kernel clocks (mgx_set_clock, ABI 6): every launch of the step kernels (class 0: mgx_step,
+        mgx_step_compact, mgx_rollout_compact) and of the refill (class 1) records its span, first workgroup
+        start to last workgroup end, on the device -- so a launch inside a replayed hipGraph is timed where it
+        runs.  Set before capturing graphs (kernel parameters are captured)."""
+        blk = _lib.CLOCK_HDR + 2 * int(slots)
+        self.clock = torch.zeros(_lib.CLOCK_CLASSES * blk, dtype=torch.int64, device=self.device)
+        khz = ctypes.c_int(0)
+        _lib.check(self.L.mgx_set_clock(self.h, _ptr(self.clock), int(slots), ctypes.byref(khz)), "mgx_set_clock")
+        self.clock_slots, self.clock_khz = int(slots), int(khz.value)
+        return self.clock
+
+    def clock_launches(self, cls=0):
+        """Launches of kernel class `cls` recorded so far (synchronises)."""
+        torch.cuda.synchronize(self.device)
+        return int(self.clock[cls * (_lib.CLOCK_HDR + 2 * self.clock_slots)])
+
+    def clock_spans_us(self, cls, first, last):
+        """Durations (us) of launches [first, last) of kernel class `cls` (synchronises)."""
+        import numpy as np
+        torch.cuda.synchronize(self.device)
+        b = cls * (_lib.CLOCK_HDR + 2 * self.clock_slots) + _lib.CLOCK_HDR
+        last = min(last, self.clock_slots)
+        if last <= first:
+            return []
+        v = self.clock[b + 2 * first:b + 2 * last].cpu().numpy().view(np.uint64).reshape(-1, 2)
+        start, end = ~v[:, 0], v[:, 1]
+        return [float(e - s_) * 1e3 / self.clock_khz for s_, e in zip(start, end)]
+
     def join(self):
         """Make the current stream wait for the in-flight episode refill (mgx_join)."""
         _lib.check(self.L.mgx_join(self.h, self._stream()), "mgx_join")
@@ -206,11 +235,23 @@ class MgxEngine:
             pass
 
 
+def _check_stats(stats, device=None):
+    """The adv-stat triple: f64, >= 3 elements, contiguous, on `device` (the kernel adds to stats[0..2])."""
+    if stats is None:
+        return
+    if stats.dtype != torch.float64 or stats.numel() < 3 or not stats.is_contiguous() or not stats.is_cuda \
+            or (device is not None and stats.device != torch.device(device)):
+        raise ValueError("stats must be a contiguous f64 tensor of >= 3 elements on %s" % (device or "the GPU"))
+
+
 def _scratch_for(stats, scratch):
+    _check_stats(stats)
     if scratch is None:
         return _stats_scratch(stats)
-    assert stats is not None and scratch.dtype == torch.float64 and scratch.is_contiguous() \
-        and scratch.numel() >= _lib.GAE_SCRATCH_WORDS and scratch.device == stats.device
+    if stats is None or scratch.dtype != torch.float64 or not scratch.is_contiguous() \
+            or scratch.numel() < _lib.GAE_SCRATCH_WORDS or scratch.device != stats.device:
+        raise ValueError("scratch must be a contiguous f64 tensor of >= %d elements on the stats' device"
+                         % _lib.GAE_SCRATCH_WORDS)
     return scratch
 
 

@@ -185,7 +185,7 @@ class CompactRollout:
     + mission id per env-step, stacks rebuilt by mgx_gather), per-step policy outputs, GAE."""
 
     def __init__(self, engine, T):
-        self.buf = CompactBuffer(engine, T)
+        self.buf = CompactBuffer(engine, T, ring=True)      # history rows read in place (no per-rollout copy)
         self.T, self.N = T, engine.n
         dev = engine.device
         self.actions = torch.zeros((T, self.N), dtype=torch.int64, device=dev)
@@ -208,11 +208,11 @@ class CompactRollout:
     def minibatches(self, batch_size, perm):
         """perm: permutation of the env-major flat index i = env * T + t (SB3 swap_and_flatten);
         observations gathered straight into the policy's f32 input."""
-        T, N, H = self.T, self.N, self.buf.H
+        T = self.T
         for s in range(0, perm.numel(), batch_size):
             idx = perm[s:s + batch_size]
             env, t = idx // T, idx % T
-            obs = self.buf.gather((H + t) * N + env, f32=True)
+            obs = self.buf.gather(self.buf.index(t, env), f32=True)
             yield (obs, self.actions[t, env], self.values[t, env], self.log_probs[t, env],
                    self.advantages[t, env], self.returns[t, env])
 

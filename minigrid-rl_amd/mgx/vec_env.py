@@ -84,9 +84,10 @@ class MgxVecEnv(_VecEnvBase):
             # recurrent (environment.py:28-29); otherwise the env hands out MiniGridEnv's Discrete(4)
             self.dir_one_hot = int(n_frames_stack) > 1 and not recurrent
         else:
-            if recurrent:
+            if recurrent or int(n_frames_stack) <= 1:
                 raise ValueError("fused mode is VecTransposeImage + VecFrameStack, which the reference applies only "
-                                 "when not recurrent (ppo.py:124): use raw=True")
+                                 "when n_frames_stack > 1 and not recurrent (ppo.py:124, environment.py:28): "
+                                 "use raw=True")
             self.dir_one_hot = True
         if vec_env_cls not in ("subproc", "dummy"):
             raise ValueError("vec_env_cls must be 'subproc' or 'dummy'")
@@ -196,10 +197,11 @@ class MgxVecEnv(_VecEnvBase):
         raise AttributeError("per-env methods are not exposed (%s)" % method_name)
 
     def env_is_wrapped(self, wrapper_class, indices=None):
-        # Every env is Monitor-wrapped (make_vec_env) with TokenizeVocab/Discrete2Box inside
         name = getattr(wrapper_class, "__name__", str(wrapper_class))
-        return [name in ("Monitor", "TokenizeVocabWrapper", "Discrete2BoxWrapper")
-                for _ in self._indices(indices)]
+        # Every env is Monitor-wrapped (make_vec_env) with TokenizeVocabWrapper inside; Discrete2BoxWrapper only
+        # where make_env adds it (n_frames_stack > 1 and not recurrent, environment.py:28-29)
+        wrapped = ("Monitor", "TokenizeVocabWrapper") + (("Discrete2BoxWrapper",) if self.dir_one_hot else ())
+        return [name in wrapped for _ in self._indices(indices)]
 
     def get_images(self):
         raise NotImplementedError("rendering is outside the engine's scope (DESIGN.md §9)")

@@ -76,38 +76,51 @@ def test_gathered_stacks_equal_materialised_stacks(case):
         assert np.array_equal(a_[key], b_[key]), key
 
 
-def test_carry_over_and_minibatch_gather():
-    """Two rollouts of T=8 with the buffer carried over: any (t, env) sample of the second
-    rollout, in a random minibatch order, gathers the stack the SB3 engine showed at that step
-    (the history rows bridge the rollout boundary)."""
+@pytest.mark.parametrize("ring,T,rolls", [(False, 8, 2), (True, 8, 4), (True, 2, 7), (True, 3, 5)],
+                         ids=["copy_T8", "ring_T8", "ring_T2", "ring_T3"])
+def test_carry_over_and_minibatch_gather(ring, T, rolls):
+    """Rollouts of T steps with the buffer carried over: any (t, env) sample of every rollout after the
+    first, in a random minibatch order, gathers the stack the SB3 engine showed at that step (the history
+    rows bridge the rollout boundary).  ring=True (the bench's and the collector's layout): the history rows
+    are read in place through mgx_gather_ring, the ring wraps several times (T = 2 and 3 < n_stack: the
+    history reaches two blocks back), and the terminal stacks of the finished episodes are checked too."""
     _need_gpu()
     from mgx import MgxEngine
     from mgx.compact import CompactBuffer
-    n, T = 96, 8
-    ref = MgxEngine(problem="multi", mission=None, size=8, n_envs=n, mission_dtype=torch.uint8)
-    cmp_ = MgxEngine(problem="multi", mission=None, size=8, n_envs=n, mission_dtype=torch.uint8)
-    buf = CompactBuffer(cmp_, T)
+    n = 96
+    ref = MgxEngine(problem="multi", mission=None, size=8, n_envs=n, mission_dtype=torch.uint8, terminal_mode="all")
+    cmp_ = MgxEngine(problem="multi", mission=None, size=8, n_envs=n, mission_dtype=torch.uint8, terminal_mode="all")
+    buf = CompactBuffer(cmp_, T, ring=ring)
     ref.reset()
     cmp_.reset()
     buf.observe(0)
     g = torch.Generator(device="cuda")
     g.manual_seed(3)
-    for roll in range(2):
+    for roll in range(rolls):
+        if roll:
+            buf.carry_over()
         seen = []
         for t in range(T):
             seen.append({k: v.clone() for k, v in ref.obs.items()})
             a = torch.randint(0, 7, (n,), device="cuda", generator=g)
+            if t % 5 == 4:
+                a[: n // 3] = 6                                  # bursts of 'done'
             ref.step(a)
             buf.step(t, a)
+            assert torch.equal(buf.dones[t].bool(), ref.done), (roll, t)
+            d = ref.done.nonzero().flatten()
+            if d.numel():
+                gt = buf.gather_step(t, terminal=True, f32=False, envs=d)
+                for key in ("image", "direction", "mission"):
+                    assert torch.equal(gt[key], ref.terminal_obs[key][d]), (roll, t, key)
         if roll == 0:
-            buf.carry_over()
             continue
         perm = torch.randperm(n * T, device="cuda")            # env-major flat index (swap_and_flatten)
         env, t_ = perm // T, perm % T
-        got = buf.gather((buf.H + t_) * n + env, f32=False)
+        got = buf.gather(buf.index(t_, env), f32=False)
         for key in ("image", "direction", "mission"):
             want = torch.stack([seen[int(tt)][key][int(ee)] for tt, ee in zip(t_.tolist(), env.tolist())])
-            assert torch.equal(got[key], want), key
+            assert torch.equal(got[key], want), (roll, key)
 
 
 def test_graph_replays_equal_eager_steps():

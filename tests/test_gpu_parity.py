@@ -387,9 +387,10 @@ def test_full_size_matches_oracle(problem, mission, size, n, T, layout):
 @pytest.mark.parametrize("n", [8192, 65536])
 def test_bench_shape_graph_matches_oracle(n, layout):
     """The exact shape bench.py times -- the driver's `--steps 20` line: GTG 8x8, terminal_mode
-    'truncated', refill epoch E = 20 = horizon H, one hipGraph per chunk holding the carry-over, the
-    steps, mgx_gae_dones with the adv-stat triple and mgx_join -- replayed 4 times with new actions in
-    its static buffer.  `fused` (the headline): ONE mgx_rollout_compact launch of the 20 steps (it
+    'truncated', refill epoch E = 20 = horizon H, the compact buffer as a ring of two 20-row blocks (round 5:
+    the carry-over is a block advance, no copy) and so two hipGraphs, one per block, each holding the
+    carry-over, the steps, mgx_gae_dones with the adv-stat triple and mgx_join -- replayed in turn 4 times
+    with new actions in their static buffer.  `fused` (the headline): ONE mgx_rollout_compact launch of the 20 steps (it
     forks the epoch's refill); `fused_gae`: the same launch with the GAE fused in (mgx_rollout_compact_gae,
     the bench's graph at E = H); `compact`: 20 mgx_step_compact launches (the per-step line).  Every
     replay: each step's observation rows, mission ids, dones, terminated / truncated flags and f32
@@ -406,8 +407,7 @@ def test_bench_shape_graph_matches_oracle(n, layout):
                     refill_every=E)
     assert eng.refill_every == E
     dev = eng.device
-    buf = CompactBuffer(eng, E)
-    H = buf.H
+    buf = CompactBuffer(eng, E, ring=True)
     tok = mission_tokens()
     rng = np.random.default_rng(77)
     acts = rng.integers(0, 7, (W + reps * E, n)).astype(np.int32)
@@ -434,28 +434,33 @@ def test_bench_shape_graph_matches_oracle(n, layout):
     static = torch.zeros((E, n), dtype=torch.int32, device=dev)
     gamma, lam = 0.8108071290665859, 0.9452281119742252
     s = torch.cuda.Stream()
+    c0, graphs = buf.c, []
     with torch.cuda.stream(s):
-        gr = torch.cuda.CUDAGraph()
-        gr.capture_begin()
-        st.zero_()
-        buf.carry_over()
-        if layout == "fused_gae":
-            buf.rollout(0, static, gae=dict(values=vals, last_values=last_v, gamma=gamma, gae_lambda=lam,
-                                            out=(adv, ret), stats=st))
-        elif fused:
-            buf.rollout(0, static)
-        else:
-            for j in range(E):
-                buf.step(j, static[j])
-        if layout != "fused_gae":
-            gae_dones(buf.rewards, vals, buf.dones, last_v, gamma, lam, stats=st, out=(adv, ret))
-        eng.join()
-        gr.capture_end()
+        for _ in range(buf.blocks):                 # one graph per ring block, as bench.py captures them
+            gr = torch.cuda.CUDAGraph()
+            gr.capture_begin()
+            st.zero_()
+            buf.carry_over()
+            if layout == "fused_gae":
+                buf.rollout(0, static, gae=dict(values=vals, last_values=last_v, gamma=gamma, gae_lambda=lam,
+                                                out=(adv, ret), stats=st))
+            elif fused:
+                buf.rollout(0, static)
+            else:
+                for j in range(E):
+                    buf.step(j, static[j])
+            if layout != "fused_gae":
+                gae_dones(buf.rewards, vals, buf.dones, last_v, gamma, lam, stats=st, out=(adv, ret))
+            eng.join()
+            gr.capture_end()
+            graphs.append(gr)
     torch.cuda.synchronize()
+    assert buf.blocks == 2
     for r in range(reps):
         static.copy_(torch.as_tensor(acts[W + r * E:W + (r + 1) * E], device=dev))
-        gr.replay()
+        graphs[r % buf.blocks].replay()
         torch.cuda.synchronize()
+        b0 = ((c0 + r % buf.blocks + 1) % buf.blocks) * E      # the block this replay wrote: obs j+1 at b0 + j
         rows = buf.rows.cpu().numpy()
         mids = buf.mids.cpu().numpy()
         starts = buf.starts.cpu().numpy().astype(bool)
@@ -466,13 +471,13 @@ def test_bench_shape_graph_matches_oracle(n, layout):
         for j in range(E):
             o = ov.step(acts[W + r * E + j])
             done = (o["terminated"] | o["truncated"]).astype(bool)
-            row = rows[H + 1 + j]
+            row = rows[b0 + j]
             img = row[:, 1:].reshape(n, 3, 7, 7).transpose(0, 2, 3, 1)
             want_img = np.where(done[:, None, None, None], o["r_image"], o["image"])
             assert np.array_equal(img, want_img), (r, j, "image")
             assert np.array_equal(row[:, 0], np.where(done, o["r_dir"], o["dir"])), (r, j, "dir")
-            assert np.array_equal(tok[mids[H + 1 + j]], np.where(done[:, None], o["r_mission"], o["mission"])), (r, j)
-            assert np.array_equal(starts[H + 1 + j], done), (r, j, "done")
+            assert np.array_equal(tok[mids[b0 + j]], np.where(done[:, None], o["r_mission"], o["mission"])), (r, j)
+            assert np.array_equal(starts[b0 + j], done), (r, j, "done")
             assert np.array_equal(trm[j], o["terminated"]) and np.array_equal(trc[j], o["truncated"]), (r, j)
             assert np.array_equal(rew[j], o["reward"].astype(np.float32)), (r, j, "reward")
             tr = o["truncated"].astype(bool) & ~o["terminated"].astype(bool)
@@ -481,7 +486,7 @@ def test_bench_shape_graph_matches_oracle(n, layout):
         trows = buf.terminal_rows.cpu().numpy()
         got_t = trows[:, 1:].reshape(n, 3, 7, 7).transpose(0, 2, 3, 1)
         assert np.array_equal(got_t[t_has], t_img[t_has]), (r, "terminal rows")
-        dn = starts[H + 1:H + 1 + E]
+        dn = starts[b0:b0 + E]
         es = np.zeros((E, n), np.float32)
         es[1:] = dn[:-1]
         want_a, want_r = O.gae(rew, vals.cpu().numpy(), es, last_v.cpu().numpy(), dn[-1], gamma, lam)

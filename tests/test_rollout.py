@@ -351,3 +351,51 @@ def test_shards_equal_slices_of_one_engine(problem, mission, size, n, layout):
             assert np.array_equal(np.asarray(b[k]), np.asarray(a[k])[r * n:(r + 1) * n], equal_nan=True), (r, k)
         tot += shards[r].stats()["resets"]
     assert tot == whole.stats()["resets"]
+
+
+def test_kernel_clock_records_every_launch():
+    """mgx_set_clock (the bench's roofline timer): every step-kernel launch (fused rollout or per step) and
+    every refill launch records one span on the device, graph replays included; each span is positive and
+    lies inside the HIP-event window around its launches; clocked and unclocked engines step identically."""
+    _need_gpu()
+    from mgx import MgxEngine
+    from mgx.compact import CompactBuffer
+    n, E = 4096, 16
+    kw = dict(problem="multi", mission=5, size=8, n_envs=n, refill_every=E, mission_dtype=torch.uint8)
+    a, b = MgxEngine(**kw), MgxEngine(**kw)
+    a.enable_clock(slots=64)
+    ba, bb = CompactBuffer(a, E, ring=True), CompactBuffer(b, E, ring=True)
+    a.reset(); b.reset()
+    assert a.clock_launches(1) == 1                          # mgx_reset's synchronous fill
+    ba.observe(0); bb.observe(0)
+    acts = torch.randint(0, 7, (3 * E, n), device=a.device, dtype=torch.int32)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    ba.rollout(0, acts[:E]); bb.rollout(0, acts[:E])
+    ev1.record()
+    for t in range(E):                                       # a second epoch, one launch per step
+        ba.step(t, acts[E + t]); bb.step(t, acts[E + t])
+    a.join()                                                 # (no dependency across the capture)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin()
+        ba.rollout(0, acts[2 * E:])
+        a.join()
+        g.capture_end()
+    g.replay()
+    for t in range(E):
+        bb.step(t, acts[2 * E + t])
+    a.join()
+    torch.cuda.synchronize()
+    assert a.clock_launches(0) == 1 + E + 1
+    assert a.clock_launches(1) == 1 + 3
+    spans = a.clock_spans_us(0, 0, a.clock_launches(0))
+    assert all(0 < x < 1e5 for x in spans), spans
+    assert spans[0] <= ev0.elapsed_time(ev1) * 1e3 + 1.0, (spans[0], ev0.elapsed_time(ev1))
+    assert all(0 < x < 1e6 for x in a.clock_spans_us(1, 0, 4))
+    assert torch.equal(ba.rows, bb.rows) and torch.equal(ba.starts, bb.starts)
+    sa, sb = a.dump_state(), b.dump_state()
+    for k in ("grid", "agent", "mtwords", "pcg"):
+        assert np.array_equal(sa[k], sb[k]), k
