@@ -457,9 +457,6 @@ def measure_rollout(args, layout, world, rank, dev):
     eng = MgxEngine(problem=args.problem, mission=mission, size=args.size, n_envs=n, seed=42,
                     env_index_offset=rank * n, n_stack=args.n_stack, terminal_mode="truncated", device=dev,
                     refill_every=E or 0, refill_cap=args.refill_cap, ring_depth=args.ring_depth)
-    # device kernel clocks (mgx_set_clock): every step-kernel and refill launch records its own span, so the
-    # roofline prices the kernel's launches INSIDE the timed graph replays (set before any capture)
-    eng.enable_clock()
     E = eng.refill_every
     H = pick_horizon(K, E if aligned else None, args.horizon or 0)
     # warm-up: whole refill epochs, and at least --min-warmup (256) steps.  mgx_reset fills every ring
@@ -467,6 +464,10 @@ def measure_rollout(args, layout, world, rank, dev):
     # episode at step 0, and the reset rate (what the refill pays for) settles only after a few
     # max_steps (64 at S = 8): a window right after the reset would see fewer resets than steady state
     W = -(-max(args.warmup, args.min_warmup, 1) // E) * E
+    # device kernel clocks (mgx_set_clock): every step-kernel and refill launch records its own span, so the
+    # roofline prices the kernel's launches INSIDE the timed graph replays (set before any capture)
+    per0 = E if layout == "fused" and aligned else 1
+    eng.enable_clock(slots=(W + 3 * K + args.probe) // per0 + 64)     # every step-kernel launch of this run
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     P = args.probe
@@ -571,7 +572,7 @@ def measure_rollout(args, layout, world, rank, dev):
     st0 = eng.stats()
     # refill launches inside the timed region: the forks the steps enqueued (captured once in the
     # graphs, replayed once each; eagerly, counted as they run)
-    forks = (st0["refill_launches"] - forks0) if graphs else None
+    forks = (st0["refill_launches"] - forks0) * nchunks // len(graphs) if graphs else None
     hist.zero_()                                         # (the untimed replays accumulated into it)
     clk0 = (eng.clock_launches(0), eng.clock_launches(1))    # kernel-clock launch counts at the region's start
     if world > 1:

@@ -298,17 +298,19 @@ mgx_status mgx_rollout_compact_gae(mgx_handle *h, const int32_t *actions_dev, in
 #define MGX_SCENE_WORDS 104
 mgx_status mgx_scene(mgx_handle *h, int64_t env, uint32_t *record, void *stream);
 
-/* Kernel clocks (measurement; ABI 6).  With clock_dev set, every launch of the step kernels
- * (mgx_step, mgx_step_compact, mgx_rollout_compact[_gae]: class 0) and of the refill kernel (class 1)
- * records on the device the span from its first workgroup's start to its last workgroup's end, so
- * that a caller can time the kernels INSIDE a replayed hipGraph, beside whatever runs concurrently
- * (bench.py: the timed region's own launches).  clock_dev: u64 [MGX_CLOCK_CLASSES][MGX_CLOCK_HDR +
- * 2 * slots], caller-owned, zeroed.  Per class: [0] launches so far, [1] internal, then for launch
- * i < slots: [MGX_CLOCK_HDR + 2i] = ~start, [MGX_CLOCK_HDR + 2i + 1] = end (wall-clock ticks;
- * *tick_khz, optional, receives their rate).  Kernel parameters are captured at launch: set the clock
+/* Kernel clocks (measurement; ABI 6).  With clock_dev set, every workgroup of every launch of the step
+ * kernels (mgx_step, mgx_step_compact, mgx_rollout_compact[_gae]: class 0) and of the refill kernel
+ * (class 1) records its start and end on the device (wall-clock ticks; *tick_khz, optional, receives
+ * their rate), so that a caller can time the kernels INSIDE a replayed hipGraph, beside whatever runs
+ * concurrently (bench.py: the timed region's own launches); a launch's span is the min start to the
+ * max end over its workgroups.  clock_dev: u64 [mgx_clock_words(h, slots)], caller-owned, zeroed;
+ * per class c (G = mgx_clock_groups(h, c) workgroups per launch), in order: cnt u64 [G] (launches so
+ * far, per workgroup), then rec u64 [slots][G][2] {start, end} of launches 0 .. slots-1 (later
+ * launches are counted, not recorded).  Kernel parameters are captured at launch: set the clock
  * before capturing a graph.  NULL clock_dev: off (the default). */
 #define MGX_CLOCK_CLASSES 2
-#define MGX_CLOCK_HDR 4
+int64_t mgx_clock_words(const mgx_handle *h, int slots);
+int mgx_clock_groups(const mgx_handle *h, int cls);
 mgx_status mgx_set_clock(mgx_handle *h, uint64_t *clock_dev, int slots, int *tick_khz);
 
 /* Synchronises `stream`, returns the device error bits (MGX_DEVERR_*) and clears them. */

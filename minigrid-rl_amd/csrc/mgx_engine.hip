@@ -88,6 +88,20 @@ constexpr int SLIDE_THREADS = 256, SLIDE_ENVS = 16 * SLIDE_THREADS;
 // LDS bytes per resetting lane: MT window + objs list (obj_stride words, see mgx_create)
 __host__ __device__ constexpr int scratch_per_env(int obj_stride, int nw) { return win_stride_of(nw) * 4 + obj_stride * 4; }
 
+// ---- kernel clocks (mgx_set_clock; include/mgx.h).  Each launch of a clocked kernel records, per workgroup,
+// its start and end in wall-clock ticks (s_memrealtime), so that a caller can time a kernel INSIDE a replayed
+// hipGraph, beside whatever runs concurrently (bench.py's roofline: the timed region's own launches, not an eager
+// probe); the launch's span is the min start to the max end over its workgroups.  No atomics: workgroup b of
+// every launch of a class is the only writer of its own launch counter cnt[b] (every launch of a class has the
+// same grid) and of its record of launch cnt[b] -- plain stores, one 16-B record per workgroup (a first version
+// reduced with device-scope atomics on one address per launch and cost the 1,024-workgroup step kernel 48 us).
+// Class block (u64): cnt[G], then [slots][G] records {start, end}; G = the class's grid (mgx_clock_groups).
+enum { CLK_STEP = 0, CLK_REFILL = 1, CLK_CLASSES = 2 };
+struct KClock {
+    unsigned long long *base[CLK_CLASSES];   // per class: cnt[G] then rec[slots][G][2]
+    int groups[CLK_CLASSES];
+    int slots;
+};
 struct KParams {
     EnvState *state;
     uint8_t *grid;
@@ -144,38 +158,17 @@ struct KParams {
                             // 1 the wave's mean deficit (<= cap), 2 its mean consumption, rounded up
     uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
                             //        generation (mgx_scene regenerates it), else null
-    unsigned long long *clk;  // mgx_set_clock: per kernel class [CLK_HDR + 2 * clk_slots] launch spans, or null
-    int clk_slots;
+    KClock clk;             // mgx_set_clock: kernel clocks (clk.slots == 0: off)
 };
 
-// ---- kernel clocks (mgx_set_clock; include/mgx.h).  Each launch of a clocked kernel records the span from its
-// first workgroup's start to its last workgroup's end in wall-clock ticks (s_memrealtime), so that a caller can
-// time a kernel INSIDE a replayed hipGraph, beside whatever runs concurrently (bench.py's roofline: the timed
-// region's own launches, not an eager probe).  Class block: [0] launches so far, [1] workgroups of the running
-// launch that have finished, [2..3] unused, then per launch i < slots: [CLK_HDR + 2i] = ~(first start) (a max
-// of complements, so that a zeroed block works), [CLK_HDR + 2i + 1] = last end.  One thread per workgroup; the
-// launch's last workgroup (fenced counter) advances [0] -- every workgroup read it before that.
-constexpr int CLK_HDR = 4;
-enum { CLK_STEP = 0, CLK_REFILL = 1, CLK_CLASSES = 2 };
-__device__ __forceinline__ unsigned long long *clk_block(const KParams &p, int cls) {
-    return p.clk + (size_t)cls * (size_t)(CLK_HDR + 2 * p.clk_slots);
-}
-__device__ __forceinline__ void clk_begin(const KParams &p, int cls) {   // one thread per workgroup
-    unsigned long long *c = clk_block(p, cls);
-    const unsigned long long t = (unsigned long long)wall_clock64();
-    const unsigned long long seq = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (seq < (unsigned long long)p.clk_slots) atomicMax(&c[CLK_HDR + 2 * seq], ~t);
-}
-__device__ __forceinline__ void clk_end(const KParams &p, int cls) {     // one thread per workgroup, at its end
-    unsigned long long *c = clk_block(p, cls);
-    const unsigned long long t = (unsigned long long)wall_clock64();
-    const unsigned long long seq = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (seq < (unsigned long long)p.clk_slots) atomicMax(&c[CLK_HDR + 2 * seq + 1], t);
-    __threadfence();
-    if (atomicAdd(&c[1], 1ull) == (unsigned long long)gridDim.x - 1ull) {   // the launch's last workgroup
-        atomicExch(&c[1], 0ull);
-        atomicExch(&c[0], seq + 1ull);
-    }
+__device__ __forceinline__ unsigned long long clk_now() { return (unsigned long long)wall_clock64(); }
+__device__ __forceinline__ void clk_record(const KClock &k, int cls, unsigned long long t0) {   // one thread
+    unsigned long long *c = k.base[cls];
+    const int G = k.groups[cls], b = (int)blockIdx.x;
+    const unsigned long long i = c[b];
+    if (i < (unsigned long long)k.slots)
+        reinterpret_cast<ulonglong2 *>(c + G)[i * (unsigned long long)G + b] = make_ulonglong2(t0, clk_now());
+    c[b] = i + 1ull;
 }
 
 struct KOut {
@@ -686,7 +679,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     const int ne = (int)min<int64_t>(BLOCK_ENVS, p.n - e0);
     const int S = SC > 0 ? SC : p.S;
     if (tid == 0) s_ll = 0;
-    if (p.clk && tid == 0) clk_begin(p, CLK_STEP);
+    __shared__ unsigned long long s_t0;           // kernel clock: this workgroup's start
+    if (p.clk.slots && tid == 0) s_t0 = clk_now();
     // issue priority over the refill's waves on the same SIMD (MGX_STEP_PRIO; wave-uniform)
     if (p.step_prio == 1) __builtin_amdgcn_s_setprio(1);
     else if (p.step_prio == 2) __builtin_amdgcn_s_setprio(2);
@@ -1188,9 +1182,9 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
 #endif
 #endif
     }
-    if (p.clk) {                                  // every wave of the workgroup is done
+    if (p.clk.slots) {                            // every wave of the workgroup is done
         __syncthreads();
-        if (tid == 0) clk_end(p, CLK_STEP);
+        if (tid == 0) clk_record(p.clk, CLK_STEP, s_t0);
     }
 }
 
@@ -1276,7 +1270,8 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     const int S = SC > 0 ? SC : p.S, D = p.D;
     const bool wave0 = tid < BLOCK_ENVS, dmaw = tid >= BLOCK_THREADS;
     const int lc = min(lane, ne - 1);
-    if (p.clk && tid == 0) clk_begin(p, CLK_STEP);
+    __shared__ unsigned long long s_t0;           // kernel clock: this workgroup's start
+    if (p.clk.slots && tid == 0) s_t0 = clk_now();
     // ---- setup: ring positions and state (waves 0 and 4), grids (waves 0-3, LDS-DMA)
     if (wave0) {
         s_st[lane] = reinterpret_cast<const uint4 *>(p.state)[e0 + lc];
@@ -1643,9 +1638,9 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         if (s_cnt[1]) atomicAdd(&p.blk[blockIdx.x].z, s_cnt[1]);
         if (s_err) atomicOr(p.err, s_err);
     }
-    if (p.clk) {                                  // every wave of the workgroup is done
+    if (p.clk.slots) {                            // every wave of the workgroup is done
         __syncthreads();
-        if (tid == 0) clk_end(p, CLK_STEP);
+        if (tid == 0) clk_record(p.clk, CLK_STEP, s_t0);
     }
 }
 
@@ -1737,7 +1732,8 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     if (p.refill_prio == 1) __builtin_amdgcn_s_setprio(1);
     else if (p.refill_prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (p.refill_prio == 3) __builtin_amdgcn_s_setprio(3);
-    if (p.clk && tid == 0) clk_begin(p, CLK_REFILL);
+    __shared__ unsigned long long s_t0;           // kernel clock: this wave's start
+    if (p.clk.slots && tid == 0) s_t0 = clk_now();
 #if MGX_REFILL_CLOCK
     const unsigned long long rc0 = __builtin_amdgcn_s_memtime();   // diagnostics: wave clocks per launch
     int rc_iters = 0;
@@ -1887,7 +1883,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         b.x = (unsigned long long)csum;
         p.blk[2 * p.nblk + blockIdx.x] = b;
         if (err) atomicOr(p.err, err);
-        if (p.clk) clk_end(p, CLK_REFILL);        // (one wave per workgroup)
+        if (p.clk.slots) clk_record(p.clk, CLK_REFILL, s_t0);   // (one wave per workgroup)
     }
 }
 
@@ -3075,11 +3071,39 @@ mgx_status mgx_set_seed(mgx_handle *h, int64_t seed) {
     return MGX_OK;
 }
 
+// grid of every launch of a clocked kernel class (the clock's per-workgroup records need one grid per class)
+static int clock_groups(const mgx_handle *h, int cls) {
+    const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
+    if (cls == CLK_STEP) return (int)nblk;
+    return (int)((h->kp.n + h->kp.refill_epw - 1) / h->kp.refill_epw);   // (64 except the S = 8 kernel's 32/16)
+}
+
+int64_t mgx_clock_words(const mgx_handle *h, int slots) {
+    if (!h || slots < 1) return -1;
+    int64_t w = 0;
+    for (int c = 0; c < CLK_CLASSES; c++) w += (int64_t)clock_groups(h, c) * (1 + 2 * (int64_t)slots);
+    return w;
+}
+
+int mgx_clock_groups(const mgx_handle *h, int cls) {
+    if (!h || cls < 0 || cls >= CLK_CLASSES) return -1;
+    return clock_groups(h, cls);
+}
+
 mgx_status mgx_set_clock(mgx_handle *h, uint64_t *clock_dev, int slots, int *tick_khz) {
     if (!h || (clock_dev && slots < 1)) return fail(MGX_ERR_INVALID, "mgx_set_clock: bad argument");
-    static_assert(CLK_CLASSES == MGX_CLOCK_CLASSES && CLK_HDR == MGX_CLOCK_HDR, "include/mgx.h clock layout");
-    h->kp.clk = reinterpret_cast<unsigned long long *>(clock_dev);
-    h->kp.clk_slots = clock_dev ? slots : 0;
+    static_assert(CLK_CLASSES == MGX_CLOCK_CLASSES, "include/mgx.h clock layout");
+    KClock &k = h->kp.clk;
+    std::memset(&k, 0, sizeof k);
+    if (clock_dev) {
+        unsigned long long *b = reinterpret_cast<unsigned long long *>(clock_dev);
+        for (int c = 0; c < CLK_CLASSES; c++) {
+            k.base[c] = b;
+            k.groups[c] = clock_groups(h, c);
+            b += (size_t)k.groups[c] * (1 + 2 * (size_t)slots);
+        }
+        k.slots = slots;
+    }
     if (tick_khz) {
         int khz = 0;
         HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));

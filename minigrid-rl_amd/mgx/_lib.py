@@ -26,8 +26,8 @@ DEVERR = {1: "MT19937 ring: a cursor left the window of the stream the device ho
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
            "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_gae_dones", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text",
            "mgx_step_compact", "mgx_rollout_compact", "mgx_rollout_compact_gae", "mgx_observe_compact", "mgx_gather",
-           "mgx_gather_ring", "mgx_scene", "mgx_set_clock")
-CLOCK_CLASSES, CLOCK_HDR = 2, 4   # == MGX_CLOCK_CLASSES, MGX_CLOCK_HDR (include/mgx.h)
+           "mgx_gather_ring", "mgx_scene", "mgx_set_clock", "mgx_clock_words", "mgx_clock_groups")
+CLOCK_CLASSES = 2   # == MGX_CLOCK_CLASSES (include/mgx.h)
 
 
 class MgxConfig(ctypes.Structure):
@@ -123,6 +123,9 @@ def load():
     L.mgx_gather.argtypes = [P, P, P, P, I64, P, I64, P, P, I, P, I, P, P]
     L.mgx_gather_ring.argtypes = [P, P, P, P, I64, I64, P, I64, P, P, I, P, I, P, P]
     L.mgx_set_clock.argtypes = [P, P, I, ctypes.POINTER(I)]
+    L.mgx_clock_words.argtypes = [P, I]
+    L.mgx_clock_words.restype = I64
+    L.mgx_clock_groups.argtypes = [P, I]
     L.mgx_scene.argtypes = [P, I64, ctypes.POINTER(ctypes.c_uint32), P]
     for name in EXPORTS:
         getattr(L, name).restype = getattr(L, name).restype or I

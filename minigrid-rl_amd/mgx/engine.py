@@ -157,34 +157,41 @@ class MgxEngine:
         c = self.calls if call is None else call
         return self.ring_depth > 0 and c % self.refill_every == 0
 
-    def enable_clock(self, slots=16384):
-        """Device kernel clocks (mgx_set_clock, ABI 6): every launch of the step kernels (class 0: mgx_step,
-        mgx_step_compact, mgx_rollout_compact) and of the refill (class 1) records its span, first workgroup
-        start to last workgroup end, on the device -- so a launch inside a replayed hipGraph is timed where it
-        runs.  Set before capturing graphs (kernel parameters are captured)."""
-        blk = _lib.CLOCK_HDR + 2 * int(slots)
-        self.clock = torch.zeros(_lib.CLOCK_CLASSES * blk, dtype=torch.int64, device=self.device)
+    def enable_clock(self, slots=4096):
+        """Device kernel clocks (mgx_set_clock, ABI 6): every workgroup of every launch of the step kernels
+        (class 0: mgx_step, mgx_step_compact, mgx_rollout_compact) and of the refill (class 1) records its start
+        and end on the device -- so a launch inside a replayed hipGraph is timed where it runs.  Set before
+        capturing graphs (kernel parameters are captured).  `slots`: launches recorded per class."""
+        words = int(self.L.mgx_clock_words(self.h, int(slots)))
+        if words <= 0:
+            raise ValueError("bad clock slots")
+        self.clock = torch.zeros(words, dtype=torch.int64, device=self.device)
         khz = ctypes.c_int(0)
         _lib.check(self.L.mgx_set_clock(self.h, _ptr(self.clock), int(slots), ctypes.byref(khz)), "mgx_set_clock")
         self.clock_slots, self.clock_khz = int(slots), int(khz.value)
+        self._clock_blocks, off = [], 0
+        for c in range(_lib.CLOCK_CLASSES):
+            g = int(self.L.mgx_clock_groups(self.h, c))
+            self._clock_blocks.append((off, g))
+            off += g * (1 + 2 * self.clock_slots)
         return self.clock
 
     def clock_launches(self, cls=0):
-        """Launches of kernel class `cls` recorded so far (synchronises)."""
+        """Launches of kernel class `cls` so far (synchronises)."""
         torch.cuda.synchronize(self.device)
-        return int(self.clock[cls * (_lib.CLOCK_HDR + 2 * self.clock_slots)])
+        return int(self.clock[self._clock_blocks[cls][0]])
 
     def clock_spans_us(self, cls, first, last):
-        """Durations (us) of launches [first, last) of kernel class `cls` (synchronises)."""
-        import numpy as np
+        """Durations (us) of launches [first, last) of kernel class `cls`: min workgroup start to max workgroup
+        end of each launch (synchronises)."""
         torch.cuda.synchronize(self.device)
-        b = cls * (_lib.CLOCK_HDR + 2 * self.clock_slots) + _lib.CLOCK_HDR
+        off, g = self._clock_blocks[cls]
         last = min(last, self.clock_slots)
         if last <= first:
             return []
-        v = self.clock[b + 2 * first:b + 2 * last].cpu().numpy().view(np.uint64).reshape(-1, 2)
-        start, end = ~v[:, 0], v[:, 1]
-        return [float(e - s_) * 1e3 / self.clock_khz for s_, e in zip(start, end)]
+        rec = self.clock[off + g:off + g * (1 + 2 * self.clock_slots)].view(self.clock_slots, g, 2)[first:last]
+        span = rec[:, :, 1].max(1).values - rec[:, :, 0].min(1).values       # (ticks < 2^63: signed is fine)
+        return [float(x) * 1e3 / self.clock_khz for x in span.cpu().tolist()]
 
     def join(self):
         """Make the current stream wait for the in-flight episode refill (mgx_join)."""

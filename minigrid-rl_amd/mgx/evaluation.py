@@ -77,6 +77,84 @@ def evaluate_policy(model, engine, n_eval_episodes=10, deterministic=True, retur
     return mean_reward, std_reward
 
 
+# minigrid OBJECT_TO_IDX['door'] (the type byte of mgx_dump_state's grid); PlaygroundEnv's multi layouts place
+# 1 / 3 / 4 doors for 2 / 3 / 4 rooms (custom_env.py:617-649, 857-928, 1299-1389)
+_DOOR = 4
+_ROOMS_BY_DOORS = {1: 2, 3: 3, 4: 4}
+TASKS = (("go to goal", "GTG"), ("go to", "GTO"), ("pick up", "PKP"), ("toggle", "TGL"), ("drop", "DRP"),
+         ("move", "MOV"))
+
+
+def task_of(mission_text):
+    """README.md:54-65's task columns from a mission text ('go to goal' before 'go to')."""
+    for prefix, name in TASKS:
+        if mission_text.startswith(prefix):
+            return name
+    return mission_text
+
+
+@torch.no_grad()
+def evaluate_test_protocol(model, engine, n_episodes=1000, deterministic=True):
+    """The reference's benchmark protocol, `test()` (src/ppo.py:185-230; README.md:54-65 "Benchmark (1k ep)"):
+    ONE env, make_vec_env(make_env, n_envs=1, seed=cfg.seed, vec_env_cls=DummyVecEnv) + VecTransposeImage +
+    VecFrameStack, and per episode
+
+        obs = vec_env.reset(); while not done: action = model.predict(obs, deterministic); obs, r, done = step
+
+    with the episode's reward summed.  `engine` must be a fresh 1-env MgxEngine of the tested config (its first
+    reset is make_vec_env's seeded one: PCG64(seed), CPython random = MT19937(seed) from PlaygroundEnv.__init__,
+    custom_env.py:82).  The single MT19937 stream advances across the episodes, so missions and room counts vary
+    from episode to episode, and every episode skips one generated episode: DummyVecEnv auto-resets the env when
+    it is done (one episode generated), and test()'s next vec_env.reset() -- unseeded, both streams continuing --
+    generates another (MgxEngine.reset after the first is that unseeded reset).
+    Returns one dict per episode: reward (f64 sum), length, success (reward > 0: the mission was completed),
+    mission_id, mission text, task (README's column), rooms (multi: 2 / 3 / 4 from the door count; else 0)."""
+    from ._lib import mission_text
+    if engine.n != 1:
+        raise ValueError("the test() protocol steps ONE env (src/ppo.py:201-206: n_envs=1)")
+    act = _act_fn(model, deterministic)
+    out, texts = [], {}
+    for _ in range(n_episodes):
+        obs = engine.reset()
+        st = engine.dump_state()
+        mid = int(st["mission_id"][0])
+        doors = int((st["grid"][0, :, :, 0] == _DOOR).sum())
+        if mid not in texts:
+            texts[mid] = mission_text(mid)
+        total, length = 0.0, 0
+        while True:
+            obs = engine.step(act(obs))
+            length += 1
+            r = engine.reward64 if engine.reward64 is not None else engine.reward.double()
+            total += float(r[0])
+            if bool(engine.done[0]):
+                break
+        out.append(dict(reward=total, length=length, success=total > 0, mission_id=mid, mission=texts[mid],
+                        task=task_of(texts[mid]), rooms=_ROOMS_BY_DOORS.get(doors, 0)))
+    return out
+
+
+def summarize_episodes(eps):
+    """Success rate overall and per (task, rooms) cell, and the cell histogram, of evaluate_test_protocol's
+    episodes."""
+    import collections
+    cells = collections.defaultdict(list)
+    for e in eps:
+        cells["%s/%d rooms" % (e["task"], e["rooms"])].append(e)
+    per_task = collections.defaultdict(list)
+    for e in eps:
+        per_task[e["task"]].append(e)
+
+    def stat(v):
+        return {"episodes": len(v), "success_rate": float(np.mean([x["success"] for x in v])),
+                "mean_reward": float(np.mean([x["reward"] for x in v])),
+                "mean_length": float(np.mean([x["length"] for x in v]))}
+    return {"overall": stat(eps), "per_task": {k: stat(v) for k, v in sorted(per_task.items())},
+            "per_cell": {k: stat(v) for k, v in sorted(cells.items())},
+            "cell_histogram": {k: len(v) for k, v in sorted(cells.items())},
+            "distinct_missions": len({e["mission_id"] for e in eps})}
+
+
 class EvalCallback:
     """SB3 EvalCallback(eval_env, best_model_save_path, eval_freq, n_eval_episodes,
     deterministic=True) for mgx.ppo.learn: every `eval_freq` vectorised steps of the

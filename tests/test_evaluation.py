@@ -124,3 +124,69 @@ def test_learn_stops_when_callback_returns_false():
     pol, hist, eng = learn(cfg, total_timesteps=4 * 256 * 16, callback=cb)
     assert len(cb.evaluations) == 1          # stopped at the first evaluation (step 8 of rollout 0)
     assert len(hist) == 0                    # the interrupted rollout is not trained on
+
+
+def protocol_oracle(cfg, n_episodes):
+    """src/ppo.py:185-230 `test()` restated over the C oracle: one env seeded cfg.seed (DummyVecEnv), per
+    episode vec_env.reset() (unseeded after the first, both streams continuing from the env's auto-reset
+    episode) and the deterministic hash policy until done; -> [(reward, length, mission text, doors)]."""
+    import oracle as O
+    v = O.OracleVec(n_envs=1, **cfg)
+    out = []
+    for i in range(n_episodes):
+        r = v.reset() if i == 0 else v.reset(seed=None)
+        doors = int((v.dump()["grid"][0, :, :, 0] == 4).sum())
+        text = v.mission(0)
+        img, d = r["image"], r["dir"]
+        total, length = 0.0, 0
+        while True:
+            o = v.step(hash_action_np(img, d))
+            length += 1
+            total += float(o["reward"][0])
+            if o["terminated"][0] or o["truncated"][0]:
+                break
+            img, d = o["image"], o["dir"]
+        out.append((total, length, text, doors))
+    return out
+
+
+def test_protocol_restatement_varies_the_cell():
+    """The reference's benchmark protocol draws a different (mission, rooms) cell per episode -- the single
+    MT19937 stream advances across episodes -- whereas the first episode of N fresh envs seeded alike is ONE
+    cell (VERDICT r4 weak #1: every env's CPython random is MT19937(seed), custom_env.py:82)."""
+    from mgx.evaluation import task_of
+    cfg = dict(problem="multi", mission=None, size=8, num_objects=4, seed=42)
+    eps = protocol_oracle(cfg, 120)
+    assert {task_of(e[2]) for e in eps} == {"GTG", "GTO", "PKP", "TGL"}            # every task
+    assert {e[3] for e in eps} == {1, 3, 4}                                          # 2, 3 and 4 rooms
+    import oracle as O
+    v = O.OracleVec(n_envs=64, **cfg)
+    v.reset()
+    assert len({task_of(v.mission(i)) for i in range(64)}) == 1                     # the flawed protocol: one
+    assert len({int((g[:, :, 0] == 4).sum()) for g in v.dump()["grid"]}) == 1       # task, one room count
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("problem,mission,size", [("multi", None, 8), ("multi", 2, 8), ("multi", 1, 11)])
+def test_evaluate_test_protocol_matches_oracle(problem, mission, size):
+    """mgx.evaluate_test_protocol (one env, reset per episode, the MT stream advancing) = the restated
+    test() over the C oracle, episode by episode: reward, length, mission and room count."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mgx import MgxEngine, evaluate_test_protocol
+    cfg = dict(problem=problem, mission=mission, size=size, num_objects=4, seed=42)
+    want = protocol_oracle(cfg, 40)
+    eng = MgxEngine(problem=problem, mission=mission, size=size, n_envs=1, seed=42, reward64=True,
+                    terminal_mode="none", mission_dtype=torch.uint8, device="cuda:0")
+
+    def policy(obs):
+        img = obs["image"][:, -3:].to(torch.int64).sum((1, 2, 3))
+        d = obs["direction"][:, -4:].argmax(1)
+        return ((img + 3 * d) % 7).to(torch.int32).contiguous()
+
+    got = evaluate_test_protocol(policy, eng, 40)
+    rooms = {1: 2, 3: 3, 4: 4}
+    for g, w in zip(got, want):
+        assert (g["reward"], g["length"], g["mission"]) == (w[0], w[1], w[2])
+        assert g["rooms"] == rooms[w[3]]
+    eng.poll_error()
