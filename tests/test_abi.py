@@ -16,7 +16,7 @@ LIB = os.path.join(ROOT, "minigrid-rl_amd", "mgx", "libmgx.so")
 
 def declared():
     src = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:mgx_status|int|const char \*)\s*(mgx_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:mgx_status|int64_t|int|const char \*)\s*(mgx_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_expected_api():
