@@ -70,6 +70,12 @@
 #ifndef MGX_ROLLOUT_FIRST    // 1: mgx_rollout_compact enqueues its rollout before the epoch's refill (0: after;
 #define MGX_ROLLOUT_FIRST 0  // round 4 A/B: rollout-first 4.0-4.2 vs 5.2-5.4 x 10^9 on the 20-step line)
 #endif
+#ifndef MGX_ROLL_LOGIC_PRIO  // fused rollout: s_setprio of wave 0 during its step logic (0: none; the block waits for it)
+#define MGX_ROLL_LOGIC_PRIO 0
+#endif
+#ifndef MGX_PUBN_ACQUIRE     // 1: the fused rollout reads ring_pubn with an agent-scope acquire (0: relaxed; A/B of the
+#define MGX_PUBN_ACQUIRE 1   // acquire's cost)
+#endif
 #ifndef MGX_SERIAL_REFILL   // refill on the caller's stream (the refill alone, for timing it)
 #define MGX_SERIAL_REFILL 0
 #endif

@@ -126,11 +126,17 @@ struct KParams {
     int manual;             // PlaygroundEnv(manual=True): 'done' ends only a completed mission (custom_env.py:325)
     uint64_t *range_cur;    // [N]     target_range of the current episode (mgx_device.h: move_range)
     uint64_t *ring_range;   // [N][D]  ... of each queued episode
-    // pre-generated episode ring (see mgx_refill_kernel)
-    uint8_t *ring_grid;     // [N][D][GS]
-    uint4 *ring_hdr;        // [N][D][3] {ax|ay<<8|dir<<16|tx<<24, ty|ta<<8|mission<<16, livelocks, 0},
-                            //           then the mission's 32 tokens (the step kernel's pop needs no lookup)
-    uint4 *ring_rng;        // [N][D][2] RNG snapshot after that episode's generation
+    // pre-generated episode ring (see mgx_refill_kernel): one REC-byte record per slot, slot = env * D + pos,
+    //   [0, GS)        the grid
+    //   [GS, GS+16)    header {ax|ay<<8|dir<<16|tx<<24, ty|ta<<8|mission<<16, livelocks, 0}
+    //   [GS+16, GS+48) RNG snapshot after that episode's generation (PCG64 state; uinteger, has, MT cursor)
+    //   then zeros to REC = roundup(GS + 48, 64): whole 64-B units, so the refill writes whole lines
+    // (round 5: one array-of-records instead of grid / header+tokens / RNG arrays -- the refill's lanes wrote
+    // their slots' 16-B pieces 16 KB apart, ~64 B of HBM write per 16-B store; the records are now written
+    // by the whole wave, consecutive lanes on consecutive pieces.  The mission tokens are no longer copied
+    // into the ring: the one reader, the SB3 layout's pop, looks them up in mtok.)
+    uint8_t *ring_rec;      // [N][D][REC]
+    int REC;
     uint4 *cur_rng;         // [N][2]   RNG snapshot after the current episode's generation
     // SPSC ring indices (rpos_t, mod 2^16; D is a power of two <= MGX_MAX_RING):
     rpos_t *ring_head;      // [N] consumer (step kernel) position
@@ -657,9 +663,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     uint4 *s_phdr = reinterpret_cast<uint4 *>(s_pgrid + BLOCK_ENVS * GS);   // popped ring slot header
     uint4 *s_tokA = s_phdr + BLOCK_ENVS;         // per lane: the current mission's tokens 0..15,
     uint4 *s_tokB = s_tokA + BLOCK_ENVS;         // 16..31 (envs whose stack is still filling)
-    uint4 *s_ptokA = s_tokB + BLOCK_ENVS;        // ... and the popped episode's mission tokens
-    uint4 *s_ptokB = s_ptokA + BLOCK_ENVS;       // (none of the four in COMPACT)
-    uint4 *s_prng = COMPACT ? s_phdr + BLOCK_ENVS : s_ptokB + BLOCK_ENVS;   // [2][64] popped RNG snapshot
+    uint4 *s_prng = COMPACT ? s_phdr + BLOCK_ENVS : s_tokB + BLOCK_ENVS;    // [2][64] popped RNG snapshot
+                                                 // (s_tokA / s_tokB: none in COMPACT)
     const int IMG = p.img_bytes;
     const int FSTRIDE = (fast || COMPACT) ? FROW : IMG, FOFF = (fast || COMPACT) ? 1 : 0;
     __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params ax | ay<<8 | dir<<16 | carry<<24
@@ -793,16 +798,12 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             }
             if (spec) {
                 const int64_t slot = (e0 + lw) * p.D + (rhead & (p.D - 1));
-                __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot, s_phdr, 16, 0, 0);
-                if (!COMPACT) {
-                    __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 1, s_ptokA, 16, 0, 0);
-                    __builtin_amdgcn_global_load_lds(p.ring_hdr + 3 * slot + 2, s_ptokB, 16, 0, 0);
-                }
-                __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot, s_prng, 16, 0, 0);
-                __builtin_amdgcn_global_load_lds(p.ring_rng + 2 * slot + 1, s_prng + BLOCK_ENVS, 16, 0, 0);
-                const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.ring_grid + slot * GS);
+                const uint4 *rec = reinterpret_cast<const uint4 *>(p.ring_rec + slot * (SC > 0 ? ((GS + 48 + 63) & ~63) : p.REC));
+                __builtin_amdgcn_global_load_lds(rec + (GS >> 4), s_phdr, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(rec + (GS >> 4) + 1, s_prng, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(rec + (GS >> 4) + 2, s_prng + BLOCK_ENVS, 16, 0, 0);
                 for (int c = 0; c < (GS >> 4); c++)
-                    __builtin_amdgcn_global_load_lds(gsrc + c, s_pgrid + c * (BLOCK_ENVS * 16), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds(rec + c, s_pgrid + c * (BLOCK_ENVS * 16), 16, 0, 0);
             }
             // (no register load here: its phi copy after the branch would wait on the DMA above)
         }
@@ -955,15 +956,16 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     // slot), then the one flipping slot of filling envs
     if (!COMPACT) {
         const int K = p.n_stack, CPS = p.mission64 ? 16 : 2, per = K * CPS;
-        const uint8_t *tA = reinterpret_cast<const uint8_t *>(s_ptokA), *tB = reinterpret_cast<const uint8_t *>(s_ptokB);
         const int tot_d = s_npop * per;
         for (int w = tid; w < tot_d; w += BLOCK_THREADS) {
             const int i = w / per, j = w - i * per;
             const int le = s_dlist[i], sl = j / CPS, c = j - sl * CPS;
-            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk2(o.mis, p.mission64, e0 + le, K, sl, c, tA + le * 16, tB + le * 16, sl != K - 1);
+            // the popped episode's tokens: its mission id (header) -> the token table (L2-resident; round 5: the
+            // ring no longer carries a copy of them)
+            const uint8_t *tk = p.mtok + ((s_phdr[le].y >> 16) & 0xFFu) * 32;
+            if (!(MGX_DIAG_SKIP & 4)) write_mission_chunk2(o.mis, p.mission64, e0 + le, K, sl, c, tk, tk + 16, sl != K - 1);
         }
-        tA = reinterpret_cast<const uint8_t *>(s_tokA);
-        tB = reinterpret_cast<const uint8_t *>(s_tokB);
+        const uint8_t *tA = reinterpret_cast<const uint8_t *>(s_tokA), *tB = reinterpret_cast<const uint8_t *>(s_tokB);
         // int64: the flipping slot (256 B, whole lines); u8: the whole row (one line at n_stack
         // 4; a 32-B slot alone would be a partial-line write)
         const int perf = p.mission64 ? CPS : per, tot_f = s_nf * perf;
@@ -1289,9 +1291,10 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     // stage ring episode h of env e (this lane's) into buffer h & 1: header, grid
     auto stage = [&](rpos_t h) {
         const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + (h & (D - 1));   // N * D < 2^32
-        const uint4 *hs = p.ring_hdr + 3 * slot;
-        // the grid's byte offset is 64-bit: N * D * GS reaches 2^33 at config 5 (131,072 x 256 x 256)
-        const uint4 *gs = reinterpret_cast<const uint4 *>(p.ring_grid + (size_t)slot * (size_t)(GSQ << 4));
+        // the record's byte offset is 64-bit: N * D * REC reaches 2^33 at config 5 (131,072 x 256 x 320)
+        const uint4 *gs = reinterpret_cast<const uint4 *>(
+            p.ring_rec + (size_t)slot * (size_t)(SC > 0 ? (((GSQ << 4) + 48 + 63) & ~63) : p.REC));
+        const uint4 *hs = gs + GSQ;
         // LDS-DMA destinations (M0) must be wave-uniform: one pass per buffer, each under the exec mask of
         // its lanes, as two separate branches -- NOT if / else.  From an if / else whose arms issue the same
         // loads to different LDS bases, the compiler sank a common load (chunk 3 at S = 8, the loop unrolled)
@@ -1323,7 +1326,8 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         // (LDS-DMA included) after it, whatever the slot lines' history in this CU's caches.  Once per env per
         // launch.
         const rpos_t rhead = p.ring_head[e0 + lane];
-        const rpos_t rpub = __hip_atomic_load(p.ring_pubn + e0 + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const rpos_t rpub = __hip_atomic_load(p.ring_pubn + e0 + lane, MGX_PUBN_ACQUIRE ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
         head0 = rhead;
         s_pub[lane] = rpub;
         const int q = (rpos_t)(rpub - rhead);
@@ -1405,7 +1409,12 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             asm volatile("" : "+v"(tidv));
             const int lanev = tidv & (BLOCK_ENVS - 1);
             if (wave0) {
-                // ---- the step: one lanev per env
+                // ---- the step: one lanev per env.  The block waits for this one wave at the post-logic barrier:
+                // MGX_ROLL_LOGIC_PRIO raises its issue priority for the phase (over the co-resident refill waves'
+                // priority 2), back to 0 for the render
+                if (MGX_ROLL_LOGIC_PRIO == 3) __builtin_amdgcn_s_setprio(3);
+                else if (MGX_ROLL_LOGIC_PRIO == 2) __builtin_amdgcn_s_setprio(2);
+                else if (MGX_ROLL_LOGIC_PRIO == 1) __builtin_amdgcn_s_setprio(1);
                 bool tw = false;
                 uint8_t popb = 0xFF;
                 uint32_t nh = NO_POP;
@@ -1480,6 +1489,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                     s_tmask = tm;
                     if (MGX_ROLL_POPCNT) s_cnt[0] += (unsigned long long)__popcll(pm);
                 }
+                if (MGX_ROLL_LOGIC_PRIO) __builtin_amdgcn_s_setprio(0);
             }
             RSTAMP(1);                                     // step logic (wave 0)
             sync_keep_vm<MGX_ROLL_VMKEEP>();
@@ -1608,8 +1618,10 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     const bool rng_w = dmaw && lane < ne && s_head[lane] != head0;
     if (rng_w) {
         const uint32_t slot = (uint32_t)(e0 + lane) * (uint32_t)D + ((rpos_t)(s_head[lane] - 1) & (D - 1));
-        rng0 = p.ring_rng[2 * slot];
-        rng1 = p.ring_rng[2 * slot + 1];
+        const uint4 *rec = reinterpret_cast<const uint4 *>(
+            p.ring_rec + (size_t)slot * (size_t)(SC > 0 ? (((GSQ << 4) + 48 + 63) & ~63) : p.REC));
+        rng0 = rec[GSQ + 1];
+        rng1 = rec[GSQ + 2];
     }
     if (dmaw) __builtin_amdgcn_s_waitcnt(0);         // the loads have returned ...
     __syncthreads();                                 // ... before wave 0 stores the heads below
@@ -1794,28 +1806,40 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
             }
         }
     }
+    int nfree = 0, nmin = 0;
     if (e < p.n) {
         // mgx_reset's fill: every ring to D (not just the invariant's 2K), so the epochs that follow
         // start at steady state: production then tracks consumption at once instead of running
         // need-driven rounds until the rings have filled (1,500+ steps at a cap near consumption)
-        int nfree = p.initial_fill ? space : max(need, p.cap < 0 ? space : min(cap, space));
+        nfree = p.initial_fill ? space : max(need, p.cap < 0 ? space : min(cap, space));
         nfree = min(nfree, space);
-        int nmin = max(need, 0);                   // what the ring invariant requires this epoch
-        if (nfree > 0) {
-            Gen<NW> G;
-            load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
-            if (SC > 0) G.S = SC;                      // (p.S == SC: the host picks this kernel for it)
+        nmin = max(need, 0);                       // what the ring invariant requires this epoch
+    }
+    const bool producer = nfree > 0;
+    if (__ballot(producer)) {
+        Gen<NW> G;
+        load_gen(G, p, e, s_grid + tid * p.GSL, s_scr, tid);
+        if (SC > 0) G.S = SC;                      // (p.S == SC: the host picks this kernel for it)
+        int livelocks = 0;
+        if (producer) {
             load_rng(G, p, e);
-            int livelocks = (int)(p.aux[e].y >> 1);   // abandoned attempts carried over from the last epoch
-            // One attempt per iteration for every lane: a lane whose attempt live-locked retries
-            // while the others already generate their next episode, exactly reset_env's retry
-            // semantics per env.  `nfree` budgets ATTEMPTS: an abandoned attempt costs the lane one
-            // episode of this epoch's production (unless the invariant needs it), not the wave an
-            // extra round -- the retry then continues in the next epoch, its count carried in aux.
-            while (nfree > 0) {
+            livelocks = (int)(p.aux[e].y >> 1);    // abandoned attempts carried over from the last epoch
+        }
+        // The lane's objs list (dead once its attempt is done) stages the episode's header + RNG snapshot for
+        // the wave's record write; its grid is already in LDS (G.g)
+        uint32_t *const stg = G.objs;
+        // One attempt per round for every lane: a lane whose attempt live-locked retries while the others
+        // already generate their next episode, exactly reset_env's retry semantics per env.  `nfree` budgets
+        // ATTEMPTS: an abandoned attempt costs the lane one episode of this epoch's production (unless the
+        // invariant needs it), not the wave an extra round -- the retry then continues in the next epoch, its
+        // count carried in aux.  The rounds are wave-uniform (the record write below needs every lane).
+        while (__ballot(nfree > 0)) {
 #if MGX_REFILL_CLOCK
-                rc_iters++;
+            rc_iters += nfree > 0;
 #endif
+            bool wrote = false;
+            uint32_t slot = 0;
+            if (nfree > 0) {
                 ResetOut R;
                 G.astart = G.cur;
                 G.abort = false;
@@ -1824,32 +1848,48 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
                 if (G.nobjs > p.obj_cap) G.err |= 8u;
                 if (G.abort && ++livelocks <= 100000) {
                     if (nfree > nmin) nfree--;
-                    continue;
+                } else {
+                    if (G.abort) G.err |= 4u;       // give up on this env (reported, never silent)
+                    R.livelocks = livelocks;
+                    livelocks = 0;
+                    nfree--;
+                    nmin--;
+                    slot = (uint32_t)e * (uint32_t)p.D + (tail & (p.D - 1));    // N * D < 2^32
+                    const uint4 h = pack_hdr(G, R);
+                    uint4 rs[2];
+                    rng_snapshot(G, rs);
+                    stg[0] = h.x; stg[1] = h.y; stg[2] = h.z; stg[3] = h.w;
+                    stg[4] = rs[0].x; stg[5] = rs[0].y; stg[6] = rs[0].z; stg[7] = rs[0].w;
+                    stg[8] = rs[1].x; stg[9] = rs[1].y; stg[10] = rs[1].z; stg[11] = rs[1].w;
+                    if (EXT && p.has_move) p.ring_range[slot] = R.range;
+                    tail++;
+                    wrote = true;
                 }
-                if (G.abort) G.err |= 4u;           // give up on this env (reported, never silent)
-                R.livelocks = livelocks;
-                livelocks = 0;
-                nfree--;
-                nmin--;
-                // the mission's tokens first: issued before any store to the ring (which the compiler
-                // must assume may alias the table), their latency overlaps the grid copy-out
-                const uint4 tok0 = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[0];
-                const uint4 tok1 = reinterpret_cast<const uint4 *>(p.mtok + R.mission_id * 32)[1];
-                const int64_t slot = e * p.D + (tail & (p.D - 1));
-                uint4 *dst = reinterpret_cast<uint4 *>(p.ring_grid + slot * p.GS);
-                for (int c = 0; c < (p.GS >> 4); c++) {
-                    const uint32_t *q = reinterpret_cast<const uint32_t *>(G.g + c * 16);
-                    dst[c] = make_uint4(q[0], q[1], q[2], q[3]);
-                }
-                p.ring_hdr[3 * slot] = pack_hdr(G, R);
-                if (!(MGX_GEN_SKIP & 64)) {                // (elimination build 64: no token copy)
-                    p.ring_hdr[3 * slot + 1] = tok0;
-                    p.ring_hdr[3 * slot + 2] = tok1;
-                }
-                rng_snapshot(G, p.ring_rng + 2 * slot);
-                if (EXT && p.has_move) p.ring_range[slot] = R.range;
-                tail++;
             }
+            // The round's records, written by the whole wave: piece j (16 B) of lane src's record by lane
+            // q % 64 of pass q / 64, q = src * P + j -- consecutive lanes store consecutive pieces, so every
+            // record (REC = 128 B at S = 8: one line) is one coalesced write
+            const unsigned long long wm = __ballot(wrote);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the lanes' LDS stages ...
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // ... before the other lanes read them
+            const int REC = SC > 0 ? ((((SC * SC + 15) & ~15) + 48 + 63) & ~63) : p.REC;
+            const int P = REC >> 4, GQ = (SC > 0 ? ((SC * SC + 15) & ~15) : p.GS) >> 4;
+            const uint8_t *objs0 = reinterpret_cast<const uint8_t *>(stg) - tid * (p.obj_stride * 4);
+            for (int q = tid; q < 64 * P; q += 64) {
+                const int src = q / P, j = q - src * P;
+                const uint32_t ss = (uint32_t)__shfl((int)slot, src);
+                if (!((wm >> src) & 1ull)) continue;
+                const uint32_t *w = j < GQ ? reinterpret_cast<const uint32_t *>(s_grid + src * p.GSL + 16 * j)
+                                           : reinterpret_cast<const uint32_t *>(objs0 + src * (p.obj_stride * 4) +
+                                                                                 16 * (j - GQ));
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (j < GQ + 3) v = make_uint4(w[0], w[1], w[2], w[3]);
+                reinterpret_cast<uint4 *>(p.ring_rec + (size_t)ss * (size_t)REC)[j] = v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // (the next round rewrites the stages)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (producer) {
             store_rng(G, p, e, (uint32_t)livelocks);
             p.ring_tail[e] = tail;                 // published by the slide that follows (ring_pubn)
             maxcur = G.cur;
@@ -2671,7 +2711,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     }
     const int D = h->cfg.ring_depth;
     {
-        size_t rs[5] = {(size_t)N * D * GS, (size_t)N * D * 48, (size_t)N * D * 32, (size_t)N * 32, (size_t)N * 5 * sizeof(rpos_t) + 64};
+        const size_t REC = (size_t)((GS + 48 + 63) & ~63);
+        size_t rs[5] = {(size_t)N * D * REC, 16, 16, (size_t)N * 32, (size_t)N * 5 * sizeof(rpos_t) + 64};
         for (int i = 0; i < 5; i++) {
             hipError_t e = hipMalloc(&h->allocs[7 + i], rs[i] ? rs[i] : 16);
             if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, std::string("hipMalloc ring: ") + hipGetErrorString(e)));
@@ -2752,7 +2793,9 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     // per wave decides how many step workgroups fit beside it on a CU.
     p.obj_cap = std::min(MAX_OBJS, cfg->problem == MGX_PROBLEM_MULTI ? 9 + 2 * cfg->num_objects
                                    : (cfg->problem == MGX_PROBLEM_FULL ? 24 : cfg->num_objects) + 1);
-    p.obj_stride = p.obj_cap | 1;
+    // (>= 12 words: the refill stages each episode's header + RNG snapshot in the lane's objs list once the
+    // attempt is done, for the wave's coalesced record write)
+    p.obj_stride = std::max(p.obj_cap, 12) | 1;
     const int nw_ = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);   // generator variant (h->nw below)
     const int scratch = BLOCK_ENVS * scratch_per_env(p.obj_stride, nw_);
     p.stk_lds = (std::max(BLOCK_ENVS * IMG, scratch) + 15) & ~15;   // reset kernel: stack area doubles as scratch
@@ -2770,9 +2813,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.vis = cfg->see_through_walls ? 0 : 1;
     p.has_move = (cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL) ? 1 : 0;
     p.manual = cfg->manual ? 1 : 0;
-    p.ring_grid = (uint8_t *)h->allocs[7];
-    p.ring_hdr = (uint4 *)h->allocs[8];
-    p.ring_rng = (uint4 *)h->allocs[9];
+    p.ring_rec = (uint8_t *)h->allocs[7];
+    p.REC = (GS + 48 + 63) & ~63;
     p.cur_rng = (uint4 *)h->allocs[10];
     p.ring_head = (rpos_t *)h->allocs[11];
     p.ring_tail = p.ring_head + N;
@@ -2826,7 +2868,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.initial_fill = 0;
     p.mission64 = cfg->mission_int64;
     h->lds_step = (size_t)p.stk_step + (size_t)BLOCK_ENVS * 2 * GS   // grids + popped grids (chunk-major)
-                  + (size_t)BLOCK_ENVS * 7 * 16;                      // + popped header, 2x2 token halves, RNG snapshot
+                  + (size_t)BLOCK_ENVS * 5 * 16;                      // + popped header, 2 token halves, RNG snapshot
     h->lds_reset = (size_t)p.stk_lds + (size_t)p.grid_lds;
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int32_t, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step));

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Builds the diagnostic variants of libmgx.so (switches: csrc/mgx_diag.h) from the current sources, in
-# parallel, next to the product library (minigrid-rl_amd/mgx/libmgx_<name>.so; git-ignored, shipped to the GPU
-# box with the tree).  Usage: bash tools/build_diag_libs.sh [name ...]  (default: all below).
+# parallel, into ab_libs/libmgx_<name>.so (git-ignored, shipped to the GPU box with the tree while they exist:
+# delete them after the A/B -- every gpurun call and the driver's runs push the whole tree).  Usage: bash tools/build_diag_libs.sh [name ...]  (default: all below).
 set -e
 cd "$(dirname "$0")/../minigrid-rl_amd"
 declare -A V=(
@@ -39,13 +39,17 @@ declare -A V=(
   [notok]="-DMGX_GEN_SKIP=64"
   [popatomic]="-DMGX_ROLL_POPCNT=0"
   [wg16_serial]="-DMGX_MT_WG1=16 -DMGX_SERIAL_REFILL=1"
+  [relaxed]="-DMGX_PUBN_ACQUIRE=0"
+  [lprio3]="-DMGX_ROLL_LOGIC_PRIO=3"
+  [lprio2]="-DMGX_ROLL_LOGIC_PRIO=2"
 )
 names=("$@")
 [ ${#names[@]} -eq 0 ] && names=("${!V[@]}")
 pids=()
 for n in "${names[@]}"; do
   [ -n "${V[$n]+x}" ] || { echo "unknown variant: $n"; exit 1; }
-  make -s -B EXTRA="${V[$n]}" OUT=mgx/libmgx_$n.so > /tmp/build_diag_$n.log 2>&1 &
+  mkdir -p ../ab_libs
+  make -s -B EXTRA="${V[$n]}" OUT=../ab_libs/libmgx_$n.so > /tmp/build_diag_$n.log 2>&1 &
   pids+=($!)
   while [ $(jobs -rp | wc -l) -ge 4 ]; do sleep 1; done
 done

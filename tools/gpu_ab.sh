@@ -15,7 +15,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   for L in $LIBS; do
     if [ "$L" = "-" ]; then LP=$R/minigrid-rl_amd/mgx/libmgx.so; else LP=$R/$L; fi
     MGX_LIB_PATH=$LP timeout -k 10 ${BENCH_TIMEOUT:-240} python bench.py $BENCH_ARGS --cpu-seconds 0 --both-layouts 0 > $O/ab_line.json 2> $O/ab_err.log || { tail -20 $O/ab_err.log; exit 1; }
-    python -c "import json,sys; d=json.load(open('$O/ab_line.json')); r=d['roofline']; print('$L', '%.3e'%d['value'], 'kern_us=%.2f'%r['avg_launch_us'], 'pipe_us=%.2f'%r['step_pipeline_us'], 'prod/cons=%s/%s'%(d['window']['episodes_produced'],d['window']['episodes_consumed']))" | tee -a $O/ab_${TAG:-x}.txt
+    python -c "import json,sys; d=json.load(open('$O/ab_line.json')); r=d['roofline']; f=r.get('refill') or {}; print('$L', '%.3e'%d['value'], 'paid=%.3e'%d.get('value_resets_paid', 0), 'kern_us=%.2f'%r['avg_launch_us'], 'refill_us=%.1f'%f.get('avg_launch_us', 0), 'pipe_us=%.2f'%r['step_pipeline_us'], 'prod/cons=%s/%s'%(d['window']['episodes_produced'],d['window']['episodes_consumed']))" | tee -a $O/ab_${TAG:-x}.txt
     python -c "import json; d=json.load(open('$O/ab_line.json')); d['lib']='$L'; print(json.dumps(d))" >> $O/ab_${TAG:-x}.jsonl
   done
 done
