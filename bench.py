@@ -574,7 +574,7 @@ def measure_rollout(args, layout, world, rank, dev):
     # graphs, replayed once each; eagerly, counted as they run)
     forks = (st0["refill_launches"] - forks0) * nchunks // len(graphs) if graphs else None
     hist.zero_()                                         # (the untimed replays accumulated into it)
-    clk0 = (eng.clock_launches(0), eng.clock_launches(1))    # kernel-clock launch counts at the region's start
+    clk0 = (eng.clock_launches(0), eng.clock_launches(1), eng.clock_launches(2))   # launch counts at the region's start
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -595,9 +595,10 @@ def measure_rollout(args, layout, world, rank, dev):
         dist.barrier()
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    clk1 = (eng.clock_launches(0), eng.clock_launches(1))
+    clk1 = (eng.clock_launches(0), eng.clock_launches(1), eng.clock_launches(2))
     timed_step_us = eng.clock_spans_us(0, clk0[0], clk1[0])      # the timed region's own kernel launches
     timed_refill_us = eng.clock_spans_us(1, clk0[1], clk1[1])
+    timed_slide_us = eng.clock_spans_us(2, clk0[2], clk1[2])
     st1 = eng.stats()
     eng.poll_error()
     # roofline probe: per-launch duration of mgx_step_kernel (HIP events on its stream) in the
@@ -723,7 +724,9 @@ def measure_rollout(args, layout, world, rank, dev):
                       "steps_per_launch": E, "episodes_per_launch": produced / max(refill_launches, 1),
                       "alg_bytes_per_launch": b_ref, "achieved": b_ref / refill_us_max / 1e3,
                       "frac": b_ref / refill_us_max / 1e3 / PEAK_HBM_GBPS, "unit": "GB/s",
-                      "note": "mgx_refill kernel launches of the timed region (device clock, beside the rollout)"}
+                      "slide_avg_launch_us": (sum(timed_slide_us) / len(timed_slide_us)) if timed_slide_us else None,
+                      "note": "mgx_refill kernel launches of the timed region (device clock, beside the rollout); "
+                              "slide: the MT slide that follows each refill on its stream (rank 0)"}
         # VecFrameStack image + direction roll (reported separately); the compact layout rolls nothing
         stack_bytes = 0 if compact else n * (441 + 588 + 12 + 16)
         out = {

@@ -300,7 +300,7 @@ mgx_status mgx_scene(mgx_handle *h, int64_t env, uint32_t *record, void *stream)
 
 /* Kernel clocks (measurement; ABI 6).  With clock_dev set, every workgroup of every launch of the step
  * kernels (mgx_step, mgx_step_compact, mgx_rollout_compact[_gae]: class 0) and of the refill kernel
- * (class 1) records its start and end on the device (wall-clock ticks; *tick_khz, optional, receives
+ * (class 1) and the MT slide after it (class 2) records its start and end on the device (wall-clock ticks; *tick_khz, optional, receives
  * their rate), so that a caller can time the kernels INSIDE a replayed hipGraph, beside whatever runs
  * concurrently (bench.py: the timed region's own launches); a launch's span is the min start to the
  * max end over its workgroups.  clock_dev: u64 [mgx_clock_words(h, slots)], caller-owned, zeroed;
@@ -308,7 +308,7 @@ mgx_status mgx_scene(mgx_handle *h, int64_t env, uint32_t *record, void *stream)
  * far, per workgroup), then rec u64 [slots][G][2] {start, end} of launches 0 .. slots-1 (later
  * launches are counted, not recorded).  Kernel parameters are captured at launch: set the clock
  * before capturing a graph.  NULL clock_dev: off (the default). */
-#define MGX_CLOCK_CLASSES 2
+#define MGX_CLOCK_CLASSES 3   /* 0 step kernels, 1 refill, 2 MT slide (the kernel that follows each refill) */
 int64_t mgx_clock_words(const mgx_handle *h, int slots);
 int mgx_clock_groups(const mgx_handle *h, int cls);
 mgx_status mgx_set_clock(mgx_handle *h, uint64_t *clock_dev, int slots, int *tick_khz);

@@ -73,6 +73,9 @@
 #ifndef MGX_ROLL_LOGIC_PRIO  // fused rollout: s_setprio of wave 0 during its step logic (0: none; the block waits for it)
 #define MGX_ROLL_LOGIC_PRIO 0
 #endif
+#ifndef MGX_SLIDE_FENCE      // 1: the MT slide orders its reductions with __threadfence() (an L2 write-back per workgroup;
+#define MGX_SLIDE_FENCE 0    // round 4), 0: by waiting for its returning atomics
+#endif
 #ifndef MGX_PUBN_ACQUIRE     // 1: the fused rollout reads ring_pubn with an agent-scope acquire (0: relaxed; A/B of the
 #define MGX_PUBN_ACQUIRE 1   // acquire's cost)
 #endif

@@ -96,7 +96,7 @@ __host__ __device__ constexpr int scratch_per_env(int obj_stride, int nw) { retu
 // same grid) and of its record of launch cnt[b] -- plain stores, one 16-B record per workgroup (a first version
 // reduced with device-scope atomics on one address per launch and cost the 1,024-workgroup step kernel 48 us).
 // Class block (u64): cnt[G], then [slots][G] records {start, end}; G = the class's grid (mgx_clock_groups).
-enum { CLK_STEP = 0, CLK_REFILL = 1, CLK_CLASSES = 2 };
+enum { CLK_STEP = 0, CLK_REFILL = 1, CLK_SLIDE = 2, CLK_CLASSES = 3 };
 struct KClock {
     unsigned long long *base[CLK_CLASSES];   // per class: cnt[G] then rec[slots][G][2]
     int groups[CLK_CLASSES];
@@ -2029,6 +2029,8 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     __shared__ int s_nsb;
     const int tid = threadIdx.x;
     MtCtl *c = p.mtc;
+    __shared__ unsigned long long s_t0;           // kernel clock: this workgroup's start
+    if (p.clk.slots && tid == 0) s_t0 = clk_now();
     unsigned long long mn = ~0ull, mx = 0;
     const int64_t e0 = (int64_t)blockIdx.x * SLIDE_ENVS;
     // Every load of the thread's 16 envs first, then the stores: with a store between them (the ring_pubn copy)
@@ -2085,16 +2087,25 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
             mn = s_red[w] < mn ? s_red[w] : mn;
             mx = s_red2[w] > mx ? s_red2[w] : mx;
         }
-        atomicMin(&c->span_min, mn);
-        atomicMax(&c->span_max, mx);
-        if (cs) atomicAdd(&c->cons_run, cs);        // (wave 0 holds every block of this workgroup)
-        __threadfence();
+        // Returning atomics, waited for: each has been performed at the device-scope coherence point when its
+        // value is back, which orders it before this workgroup's done-counter increment (round 5: with
+        // __threadfence() instead, every workgroup and the last one wrote back their XCD's whole L2 --
+        // buffer_wbl2 -- which the co-resident rollout keeps full of dirty row lines).  Everything the last
+        // workgroup reads of this pass it reads with atomics; MtCtl's plain fields come from earlier kernels.
+        const unsigned long long r0 = atomicMin(&c->span_min, mn);
+        const unsigned long long r1 = atomicMax(&c->span_max, mx);
+        const unsigned long long r2 = cs ? atomicAdd(&c->cons_run, cs) : 0ull;   // (wave 0 holds this workgroup's blocks)
+        if (MGX_SLIDE_FENCE) __threadfence();
+        else asm volatile("" ::"v"(r0), "v"(r1), "v"(r2));                     // (waits for the three returns)
         s_nsb = atomicAdd(&c->done, 1u) == gridDim.x - 1 ? 1 : -1;   // last workgroup: pass 2
     }
     __syncthreads();
-    if (s_nsb < 0) return;
+    if (s_nsb < 0) {
+        if (p.clk.slots && tid == 0) clk_record(p.clk, CLK_SLIDE, s_t0);
+        return;
+    }
     if (tid == 0) {
-        __threadfence();
+        if (MGX_SLIDE_FENCE) __threadfence();
         const unsigned long long cons = atomicExch(&c->cons_run, 0ull);   // the last refill's consumption, all envs
         c->cons_last = cons;
         if (cons && p.D > 0 && p.n > 0) {
@@ -2128,7 +2139,10 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     }
     __syncthreads();
     const int nsb = s_nsb;
-    if (nsb == 0) return;
+    if (nsb == 0) {
+        if (p.clk.slots && tid == 0) clk_record(p.clk, CLK_SLIDE, s_t0);
+        return;
+    }
     for (int i = tid; i < 624; i += SLIDE_THREADS) s_st[i] = c->st[i];
     __syncthreads();
     unsigned long long hi = s_hi;
@@ -2154,6 +2168,7 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
     if (tid == 0) {
         c->hi = hi;
         c->lo = hi > p.mt_mask + 1 ? hi - (p.mt_mask + 1) : 0;
+        if (p.clk.slots) clk_record(p.clk, CLK_SLIDE, s_t0);
     }
 }
 
@@ -3117,6 +3132,7 @@ mgx_status mgx_set_seed(mgx_handle *h, int64_t seed) {
 static int clock_groups(const mgx_handle *h, int cls) {
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
     if (cls == CLK_STEP) return (int)nblk;
+    if (cls == CLK_SLIDE) return (int)((h->kp.n + SLIDE_ENVS - 1) / SLIDE_ENVS);
     return (int)((h->kp.n + h->kp.refill_epw - 1) / h->kp.refill_epw);   // (64 except the S = 8 kernel's 32/16)
 }
 

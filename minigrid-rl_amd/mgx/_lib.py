@@ -27,7 +27,7 @@ EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mg
            "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_gae_dones", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text",
            "mgx_step_compact", "mgx_rollout_compact", "mgx_rollout_compact_gae", "mgx_observe_compact", "mgx_gather",
            "mgx_gather_ring", "mgx_scene", "mgx_set_clock", "mgx_clock_words", "mgx_clock_groups")
-CLOCK_CLASSES = 2   # == MGX_CLOCK_CLASSES (include/mgx.h)
+CLOCK_CLASSES = 3   # == MGX_CLOCK_CLASSES (include/mgx.h)
 
 
 class MgxConfig(ctypes.Structure):

@@ -42,6 +42,7 @@ declare -A V=(
   [relaxed]="-DMGX_PUBN_ACQUIRE=0"
   [lprio3]="-DMGX_ROLL_LOGIC_PRIO=3"
   [lprio2]="-DMGX_ROLL_LOGIC_PRIO=2"
+  [sfence]="-DMGX_SLIDE_FENCE=1"
 )
 names=("$@")
 [ ${#names[@]} -eq 0 ] && names=("${!V[@]}")
