@@ -420,25 +420,6 @@ __device__ __forceinline__ uint64_t win_group(Gen<NW> &G, uint64_t g) {
     return G.win[off];
 }
 __device__ __forceinline__ uint64_t div10(uint64_t v) { return __umul64hi(v, 0xCCCCCCCCCCCCCCCDull) >> 3; }
-// Wave-uniform window top-up: once some lane's window is nearly used up, every lane whose
-// window is at least half used reloads it at its current group, together: one load round
-// trip for the wave instead of one per lane at the moment its window runs out (then the
-// whole wave waits on that lane alone).  Same table words, so results are unchanged.
-template <int NW>
-__device__ __forceinline__ void mt_topup(Gen<NW> &G) {
-#if MGX_MT_TOPUP
-    constexpr int MT_WG = mt_wg<NW>();
-    const uint64_t g = G.gi;                                  // = cur / 10 (the register queue's group)
-    const int64_t used = (int64_t)(g - G.gbase);              // < 0 right after a look-ahead refill
-    if (__ballot(used >= MT_WG - MGX_MT_TOPUP)) {
-        if (used >= MT_WG / 2 && g >= G.tlo && g + MT_WG <= G.thi) {
-            GCOUNT(G, 25);
-            mt_refill_cold<MT_WG>(G.table, g & G.rmask, (lds_u64 *)G.win);
-            G.gbase = g;
-        }
-    }
-#endif
-}
 // (re)load the group registers at the current cursor
 template <int NW>
 __device__ __forceinline__ void mt_sync(Gen<NW> &G) {
@@ -1032,7 +1013,6 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     while (todo) {
         GCOUNT(G, 20);
         GSTAMP(G, 19);                                           // (commit + task advance of the previous)
-        if (!(MGX_GEN_SKIP & 16)) mt_topup(G);
         GSTAMP(G, 16);                                           // MT window top-up
         const int slot = (int)__builtin_ctzll(todo);
         const int r = slot >> 4, phase = min(slot & 15, 2);     // 0 key A, 1 key B, 2 object

@@ -34,41 +34,17 @@
 #endif
 
 // ---- A/B variants of product choices (the defaults ARE the product) ----------------------------
-#ifndef MGX_NT_STACK        // non-temporal image-stack stores in the SB3 layout
-#define MGX_NT_STACK 0
-#endif
-#ifndef MGX_SYNC_FULL       // mgx_step_kernel: full __syncthreads() instead of the LDS-only barrier
-#define MGX_SYNC_FULL 0
-#endif
-#ifndef MGX_MT_TOPUP        // wave-uniform MT window top-up at this many groups left (0: each lane reloads its
-#define MGX_MT_TOPUP 0      // window when it runs out)
-#endif
+// Retired in round 5 (settled, compiled in as the product's choice): NT_STACK 0, SYNC_FULL 0, MT_TOPUP 0,
+// STEP_S8 1, ROLL_DEFER_ROWS 1, ROLL_POPCNT 1, ROLL_S8 1, REFILL_S8 1, ROLLOUT_FIRST 0, STEP_PRIO 0,
+// REFILL_GENERIC 0, REFILL_MEAN 2, REFILL_ROUNDS 2 (their measurements: DESIGN.md §4-5).
 #ifndef MGX_MT_WG1          // MT window groups per refill lane at S <= 8 (8 or 16; 16 for larger grids)
 #define MGX_MT_WG1 8
 #endif
 #ifndef MGX_ROLL_VMKEEP      // fused rollout's two per-step barriers: -1 __syncthreads (waits for every store),
 #define MGX_ROLL_VMKEEP 8   // N >= 0: LDS complete, <= N vector-memory ops of the wave in flight, s_barrier
 #endif                      // (round 4 A/B: default line +8-10 % at 8 or 12, 20-step line within noise)
-#ifndef MGX_STEP_S8         // 1: S = 8 steps with the per-step kernel compiled for S = 8 (0: the generic one)
-#define MGX_STEP_S8 1
-#endif
-#ifndef MGX_ROLL_DEFER_ROWS  // 1: fused rollout copies step t's rows out during step t + 1's logic (waves 1-3)
-#define MGX_ROLL_DEFER_ROWS 1
-#endif
-#ifndef MGX_ROLL_POPCNT      // 1: the rollout counts a step's resets by ballot + popcount (0: an LDS atomic per pop)
-#define MGX_ROLL_POPCNT 1
-#endif
-#ifndef MGX_ROLL_S8         // 1: S = 8 runs the rollout kernel compiled for S = 8 (0: the generic one)
-#define MGX_ROLL_S8 1
-#endif
-#ifndef MGX_REFILL_S8        // 1: S = 8 refills with the kernel compiled for S = 8 (0: the generic multi one)
-#define MGX_REFILL_S8 1
-#endif
 #ifndef MGX_REFILL_EPW       // envs per S = 8 refill wave: 0 auto (32 when 64-env waves leave SIMDs idle), 16, 32, 64
 #define MGX_REFILL_EPW 0
-#endif
-#ifndef MGX_ROLLOUT_FIRST    // 1: mgx_rollout_compact enqueues its rollout before the epoch's refill (0: after;
-#define MGX_ROLLOUT_FIRST 0  // round 4 A/B: rollout-first 4.0-4.2 vs 5.2-5.4 x 10^9 on the 20-step line)
 #endif
 #ifndef MGX_ROLL_LOGIC_PRIO  // fused rollout: s_setprio of wave 0 during its step logic (0: none; the block waits for it)
 #define MGX_ROLL_LOGIC_PRIO 0
@@ -82,18 +58,6 @@
 #ifndef MGX_SERIAL_REFILL   // refill on the caller's stream (the refill alone, for timing it)
 #define MGX_SERIAL_REFILL 0
 #endif
-#ifndef MGX_STEP_PRIO       // s_setprio of the per-step kernel's waves (0..3)
-#define MGX_STEP_PRIO 0
-#endif
 #ifndef MGX_REFILL_PRIO     // s_setprio of the refill's waves over co-resident step / rollout waves (0..3)
 #define MGX_REFILL_PRIO 2
 #endif
-#ifndef MGX_REFILL_GENERIC  // 1: problem 'multi' refills with the all-problems kernel, not the multi-only one
-#define MGX_REFILL_GENERIC 0
-#endif
-#ifndef MGX_REFILL_MEAN     // per-wave production cap: 0 the fixed cfg cap, 1 the wave's mean deficit, 2 the
-#define MGX_REFILL_MEAN 2   // wave's mean consumption since its previous refill, rounded up
-#endif
-#ifndef MGX_REFILL_ROUNDS   // grid-wide ceiling of a wave's attempt rounds per epoch: 2 the Bresenham round cap
-#define MGX_REFILL_ROUNDS 2 // of mgx_mt_slide_kernel (round 4), 1 the grid's mean consumption + 1/4 rounded up
-#endif                      // (round 3), 0 none

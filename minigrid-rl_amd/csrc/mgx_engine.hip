@@ -71,7 +71,7 @@ struct MtCtl {
     // refill production ceiling (mgx_refill_kernel): the episodes every env popped between the last two
     // refill launches, summed by the slide that follows the last one (running sum, result)
     unsigned long long cons_run, cons_last;
-    // grid-wide ceiling of a refill wave's attempt rounds (MGX_REFILL_ROUNDS 2): round_cap episodes per env
+    // grid-wide ceiling of a refill wave's attempt rounds (round 4): round_cap episodes per env
     // for the next launch, from a fixed-point (1/1024) accumulator of the target production per epoch, so
     // that the ceiling alternates between floor and ceil of the target instead of always rounding up
     unsigned long long round_acc;
@@ -158,10 +158,7 @@ struct KParams {
     int cap;                // episodes an env produces per epoch beyond what the invariant needs (<0: fill to D)
     int initial_fill;       // this refill launch is mgx_reset's (fill every ring to D)
     int reset_mode;         // mgx_reset: 0 first (seeded, MT cursor 0), 1 seeded, 2 unseeded
-    int step_prio;          // s_setprio of the step kernel's waves (env MGX_STEP_PRIO, 0..3)
     int refill_prio;        // s_setprio of the refill's waves (env MGX_REFILL_PRIO, 0..3)
-    int prod_mean;          // refill production cap per wave (env MGX_REFILL_MEAN): 0 fixed `cap`,
-                            // 1 the wave's mean deficit (<= cap), 2 its mean consumption, rounded up
     uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
                             //        generation (mgx_scene regenerates it), else null
     KClock clk;             // mgx_set_clock: kernel clocks (clk.slots == 0: off)
@@ -220,17 +217,8 @@ __device__ __forceinline__ unsigned long long wave_uniform64(unsigned long long 
            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
-// Image-stack stores (diagnostic switch: -DMGX_NT_STACK = non-temporal)
-__device__ __forceinline__ void stk_store(uint4 *p, uint4 v) {
-#if MGX_NT_STACK
-    __builtin_nontemporal_store(v.x, &p->x);
-    __builtin_nontemporal_store(v.y, &p->y);
-    __builtin_nontemporal_store(v.z, &p->z);
-    __builtin_nontemporal_store(v.w, &p->w);
-#else
-    *p = v;
-#endif
-}
+// Image-stack stores
+__device__ __forceinline__ void stk_store(uint4 *p, uint4 v) { *p = v; }
 
 // Mission-stack slot writer: slot `s` of env row gets mission tokens or zeros.
 __device__ __forceinline__ void write_mission_slot(void *mis, int mission64, int64_t e, int n_stack, int s,
@@ -485,11 +473,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void mgx_reset_kernel(KParams p, KOu
 // writes are done) and s_barrier -- with a memory clobber, so that the compiler moves no memory
 // access across it.
 __device__ __forceinline__ void sync_lds() {
-#if MGX_SYNC_FULL                 // A/B builds: the full workgroup fence
-    __syncthreads();
-#else
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
 }
 
 // The fused rollout's per-step barriers (MGX_ROLL_VMKEEP >= 0): LDS complete, at most N of this wave's vector
@@ -686,10 +670,6 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     if (tid == 0) s_ll = 0;
     __shared__ unsigned long long s_t0;           // kernel clock: this workgroup's start
     if (p.clk.slots && tid == 0) s_t0 = clk_now();
-    // issue priority over the refill's waves on the same SIMD (MGX_STEP_PRIO; wave-uniform)
-    if (p.step_prio == 1) __builtin_amdgcn_s_setprio(1);
-    else if (p.step_prio == 2) __builtin_amdgcn_s_setprio(2);
-    else if (p.step_prio == 3) __builtin_amdgcn_s_setprio(3);
 #if MGX_STAMPS
     const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
     unsigned long long ts1 = 0, ts2 = 0, tsA = 0, tsB = 0, tsC = 0;
@@ -1381,7 +1361,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             __syncthreads();                                   // B: ... before the next step reads them
         }
     } else {
-        // MGX_ROLL_DEFER_ROWS: step t's frame rows are copied out by waves 1-3 during step t + 1's logic (wave 0
+        // Step t's frame rows are copied out by waves 1-3 during step t + 1's logic (wave 0
         // alone), before its post-logic barrier, instead of by every wave at the end of step t: the copy-out
         // leaves the step's critical path (the last step's rows after the loop).  s_stk is rewritten only after
         // that barrier (terminal rows, render).
@@ -1397,7 +1377,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         for (int t = 0; t < K; t++) {
             const int tb = t & 1;
             RSTAMP(0);
-            if (MGX_ROLL_DEFER_ROWS && t > 0 && !wave0) {
+            if (t > 0 && !wave0) {
                 int tq = tid;
                 asm volatile("" : "+v"(tq));
                 rows_out_block(t - 1, tq - BLOCK_ENVS, BLOCK_THREADS - BLOCK_ENVS);
@@ -1459,7 +1439,6 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                         rhead++;
                         s_head[lanev] = rhead;
                         nh = rhead;
-                        if (!MGX_ROLL_POPCNT) atomicAdd(&s_cnt[0], 1ull);
                         if (h.z) atomicAdd(&s_cnt[1], (unsigned long long)h.z);
                         lvl = (int)h.z;
                     } else {
@@ -1483,11 +1462,11 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 s_nh[tb][lanev] = nh;
                 const unsigned long long tm = __ballot(tw);
                 // resets: one popcount of the wave's pops, added by lane 0 (only wave 0 writes s_cnt), instead of
-                // a 64-bit LDS atomic per popping lane on one address (MGX_ROLL_POPCNT)
-                const unsigned long long pm = MGX_ROLL_POPCNT ? __ballot(popb != 0xFF) : 0ull;
+                // a 64-bit LDS atomic per popping lane on one address (round 4)
+                const unsigned long long pm = __ballot(popb != 0xFF);
                 if (lanev == 0) {
                     s_tmask = tm;
-                    if (MGX_ROLL_POPCNT) s_cnt[0] += (unsigned long long)__popcll(pm);
+                    s_cnt[0] += (unsigned long long)__popcll(pm);
                 }
                 if (MGX_ROLL_LOGIC_PRIO) __builtin_amdgcn_s_setprio(0);
             }
@@ -1534,25 +1513,10 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 __syncthreads();
             }
             RSTAMP(3);                                     // terminal rows + render
-            if (!MGX_ROLL_DEFER_ROWS) {
-                // rows out: per wave (its 16 rows, no barrier) or, after process_vis, per block
-                const bool wave_rows = !VIS;
-                const int r0 = wave_rows ? (tidv >> 6) * 16 : 0;
-                const int nr = wave_rows ? max(0, min(16, ne - r0)) : ne;
-                const int tt = wave_rows ? lanev : tidv, nt = wave_rows ? 64 : BLOCK_THREADS;
-                if (wave_rows) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                const int nb16 = (nr * FROW) >> 4;
-                const uint4 *src = reinterpret_cast<const uint4 *>(s_stk + r0 * FROW);
-                uint4 *dst = reinterpret_cast<uint4 *>(o.rows + ((int64_t)t * N + e0 + r0) * FROW);
-                for (int i = tt; i < nb16; i += nt) dst[i] = src[i];
-                const int rem = ((nr * FROW) >> 2) - (nb16 << 2);
-                if (tt < rem)
-                    reinterpret_cast<uint32_t *>(dst + nb16)[tt] = reinterpret_cast<const uint32_t *>(src + nb16)[tt];
-            }
             sync_keep_vm<MGX_ROLL_VMKEEP>();               // B
             RSTAMP(4);                                     // rows out + the block barrier
         }
-        if (MGX_ROLL_DEFER_ROWS && K > 0) rows_out_block(K - 1, tid, BLOCK_THREADS);   // the last step's rows
+        if (K > 0) rows_out_block(K - 1, tid, BLOCK_THREADS);   // the last step's rows
         if (o.gadv && wave0) {
             // mgx_rollout_compact_gae: mgx_gae_kernel<true>'s recurrence (same fp32 op order) for this lane's
             // env over the K steps it just ran, from the rewards / dones it wrote itself (program order), eight
@@ -1765,46 +1729,27 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
     // Production: at least what keeps >= K episodes queued at the next join (each step pops
     // <= 1, so 2K - level), plus up to `cap` more while there is room.  Capping the per-epoch
     // production balances work across the lanes of a wave (its time is the busiest lane's)
-    // while rings with slack absorb bursts of short episodes.  prod_mean: the cap is also the
-    // wave's mean deficit (D - level, rounded), so the wave runs about as many attempt rounds as
-    // its lanes consumed on average, not as many as its busiest lane did; a lane left behind
-    // keeps its deficit, which raises the next epoch's mean (the ring depth absorbs it).
-    // prod_mean 2 (default): the cap is the wave's mean CONSUMPTION since the last refill, rounded
-    // up, so the wave runs about as many attempt rounds as its lanes popped on average: production
-    // keeps up with consumption (rounding up) while the lanes that popped more than the mean keep a
-    // deficit the ring depth absorbs.  A fixed cap must sit well above the mean (rounds = cap), and
-    // the mean-deficit cap (1) settles above it too (deficits grow until the cap covers the lanes).
+    // while rings with slack absorb bursts of short episodes.  The cap is the wave's mean CONSUMPTION
+    // since the last refill, rounded up (round 3; a fixed cap must sit well above the mean, and a
+    // mean-deficit cap settles above it too), so the wave runs about as many attempt rounds as its lanes
+    // popped on average while the lanes that popped more keep a deficit the ring depth absorbs -- and at
+    // most the grid-wide round cap (round 4, below).
     int cap = p.cap;
-    if (p.prod_mean && cap > 0 && !p.initial_fill) {
-        const bool by_cons = p.prod_mean == 2;
-        int sum = e < p.n ? (by_cons ? cons : space) : 0, cnt = e < p.n ? 1 : 0;
+    if (cap > 0 && !p.initial_fill) {
+        int sum = e < p.n ? cons : 0, cnt = e < p.n ? 1 : 0;
         for (int off = 32; off > 0; off >>= 1) {
             sum += __shfl_xor(sum, off);
             cnt += __shfl_xor(cnt, off);
         }
         cnt = max(cnt, 1);
-        cap = by_cons ? (sum + cnt - 1) / cnt : min(cap, (2 * sum + cnt) / (2 * cnt));
-        if (MGX_REFILL_ROUNDS == 2 && by_cons) {
-            // The launch lasts as long as its slowest wave, and a wave runs as many attempt rounds as its
-            // cap: one ceiling common to all waves (mgx_mt_slide_kernel: the grid's mean consumption per env
-            // plus a margin, in whole rounds whose average is that target) keeps the waves whose lanes
-            // popped more than the rest from setting the launch.  Their lanes keep the difference as a
-            // deficit, which the ring depth absorbs and later epochs pay back.
-            const int rc = p.mtc->round_cap;                       // wave-uniform (scalar load)
-            if (rc > 0) cap = min(cap, rc);
-        }
-        if (MGX_REFILL_ROUNDS == 1 && by_cons) {
-            // The launch lasts as long as its slowest wave, and a wave runs as many attempt rounds as
-            // its cap: a ceiling common to all waves keeps the few waves whose lanes popped more than
-            // the rest (one in ten would round up to 6 at config 2) from setting the launch.  Their
-            // lanes keep the difference as a deficit, which the ring depth absorbs and later epochs
-            // (every wave's consumption has the same mean) pay back.
-            const unsigned long long last = p.mtc->cons_last;      // wave-uniform (scalar load)
-            if (last) {
-                const unsigned long long n4 = 4ull * (unsigned long long)p.n;
-                cap = min(cap, max(1, (int)((4ull * last + (unsigned long long)p.n + n4 - 1ull) / n4)));
-            }
-        }
+        cap = (sum + cnt - 1) / cnt;
+        // The launch lasts as long as its slowest wave, and a wave runs as many attempt rounds as its
+        // cap: one ceiling common to all waves (mgx_mt_slide_kernel: the grid's mean consumption per env
+        // plus a margin, in whole rounds whose average is that target) keeps the waves whose lanes
+        // popped more than the rest from setting the launch.  Their lanes keep the difference as a
+        // deficit, which the ring depth absorbs and later epochs pay back.
+        const int rc = p.mtc->round_cap;                           // wave-uniform (scalar load)
+        if (rc > 0) cap = min(cap, rc);
     }
     int nfree = 0, nmin = 0;
     if (e < p.n) {
@@ -2109,7 +2054,7 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
         const unsigned long long cons = atomicExch(&c->cons_run, 0ull);   // the last refill's consumption, all envs
         c->cons_last = cons;
         if (cons && p.D > 0 && p.n > 0) {
-            // Round cap of the next refill (MGX_REFILL_ROUNDS 2): target production per env per epoch =
+            // Round cap of the next refill (round 4): target production per env per epoch =
             // mean consumption + a margin m, so the lanes' levels drift up by m per epoch and only rarely
             // fall to the invariant's 2K (need-driven rounds).  A lane's deficit is a random walk with
             // per-epoch variance ~ mean (resets are ~Bernoulli per step); with drift m its stationary tail
@@ -2586,7 +2531,7 @@ struct mgx_handle {
     bool pub_stale;         // ring_pub not yet copied from ring_tail this epoch (mgx_step_kernel reads it)
     bool serial_refill;     // diagnostics (env MGX_SERIAL_REFILL=1): refill on the caller's stream
     bool refill_multi;      // problem 'multi' without EXT features refills with mgx_refill_multi_kernel
-                            // (env MGX_REFILL_GENERIC=1: the all-problems kernel, for A/B checks)
+                            // (round 2: the all-problems kernel measured the same speed)
     hipStream_t side;       // refill stream
     hipEvent_t ev_fork, ev_done;
     void *allocs[17];
@@ -2693,13 +2638,11 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->pub_stale = true;
     // scheduling choices: compile-time (mgx_diag.h; A/B builds), never read from the environment
     h->serial_refill = MGX_SERIAL_REFILL != 0;
-    h->kp.step_prio = MGX_STEP_PRIO;
     // refill waves at issue priority 2 over co-resident step / rollout waves: the refill sets the
     // pipeline beside the fused rollout (+3-7 % at config 2, +4 % at config 4; per-step layouts
     // and config 5 within +-0.5 %, round 3)
     h->kp.refill_prio = MGX_REFILL_PRIO;
-    h->kp.prod_mean = MGX_REFILL_MEAN;
-    h->refill_multi = MGX_REFILL_GENERIC == 0;
+    h->refill_multi = true;
     // MT ring: a power of two of 10-word groups holding at least mt_table_words words (>= 512 groups)
     if (h->cfg.mt_table_words <= 0) h->cfg.mt_table_words = (int64_t)1 << 26;
     int64_t ring_groups = 512;
@@ -2916,7 +2859,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
              cfg->problem == MGX_PROBLEM_MOV;
     // fewer envs per refill wave only where the S = 8 refill kernel runs (launch_refill); every other refill
     // kernel is 64 envs per wave, and the slide reads its stats by that count
-    if (!(MGX_REFILL_S8 && h->refill_multi && !h->ext && p.problem == MGX_PROBLEM_MULTI && h->nw == 1 && S == 8))
+    if (!(h->refill_multi && !h->ext && p.problem == MGX_PROBLEM_MULTI && h->nw == 1 && S == 8))
         p.refill_epw = 64;
 #define MGX_SET_LDS1(K, bytes) \
     HIP_TRY(hipFuncSetAttribute((const void *)K, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes)))
@@ -2991,7 +2934,7 @@ static mgx_status launch_refill(mgx_handle *h, void *stream, hipEvent_t done = n
     const int64_t nblk = (h->kp.n + 63) / 64;
     if (h->refill_multi && !h->ext && h->kp.problem == MGX_PROBLEM_MULTI) {
         const dim3 g((unsigned)nblk), b(64);
-        if (MGX_REFILL_S8 && h->nw == 1 && h->kp.S == 8) {
+        if (h->nw == 1 && h->kp.S == 8) {
             if (h->kp.refill_epw == 32)
                 hipLaunchKernelGGL(mgx_refill_s8_kernel<32>, dim3((unsigned)((h->kp.n + 31) / 32)), b, h->lds_refill,
                                    (hipStream_t)stream, h->kp);
@@ -3200,11 +3143,11 @@ mgx_status mgx_step(mgx_handle *h, const void *actions_dev, int action_bytes, co
         mgx_status ps = publish_for_steps(h, stream);
         if (ps != MGX_OK) return ps;
     }
-    // S = 8 (configs 2, 3 and 4): the kernel compiled for the grid size (MGX_STEP_S8)
+    // S = 8 (configs 2, 3 and 4): the kernel compiled for the grid size (round 4)
 #define MGX_STEP(A, C, SCV, LDS)                                                                                   \
     hipLaunchKernelGGL((mgx_step_kernel<A, C, SCV>), dim3((unsigned)nblk), dim3(BLOCK_THREADS), LDS, (hipStream_t)stream, \
                        h->kp, o, (const A *)actions_dev)
-    const bool s8 = MGX_STEP_S8 && h->kp.S == 8;
+    const bool s8 = h->kp.S == 8;
     if (action_bytes == 4) {
         if (s8) MGX_STEP(int32_t, false, 8, h->lds_step); else MGX_STEP(int32_t, false, 0, h->lds_step);
     } else if (action_bytes == 8) {
@@ -3251,7 +3194,7 @@ mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_b
     }
     mgx_status ps = publish_for_steps(h, stream);
     if (ps != MGX_OK) return ps;
-    const bool s8 = MGX_STEP_S8 && h->kp.S == 8;
+    const bool s8 = h->kp.S == 8;
     if (action_bytes == 4) {
         if (s8) MGX_STEP(int32_t, true, 8, h->lds_step_compact); else MGX_STEP(int32_t, true, 0, h->lds_step_compact);
     } else {
@@ -3305,12 +3248,12 @@ static mgx_status rollout_impl(mgx_handle *h, const int32_t *actions_dev, int K,
         o.gshard = gae->adv_stats_dev ? gae_scratch(gae->stats_scratch_dev) : nullptr;
     }
     // Launch order of the epoch's refill and this rollout (both start from the same fork point):
-    // MGX_ROLLOUT_FIRST.  Refill first is the default: with the rollout first, its workgroups took the CU
+    // refill first (round 4 A/B: with the rollout first, its workgroups took the CU
     // slots and the refill's waves, the longer of the two, started late (20-step line 4.0-4.2 vs
-    // 5.2-5.4 x 10^9 env-steps/s, tools/gpu_r4_refill_ab.sh), although the rollout alone is shorter then.
+    // 5.2-5.4 x 10^9 env-steps/s, tools/gpu_r4_refill_ab.sh), although the rollout alone is shorter then).
     const bool fork = h->calls % E == 0;
     if (fork) {
-        mgx_status fs = MGX_ROLLOUT_FIRST ? fork_begin(h, stream) : fork_refill(h, stream);
+        mgx_status fs = fork_refill(h, stream);
         if (fs != MGX_OK) return fs;
     }
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
@@ -3320,8 +3263,8 @@ static mgx_status rollout_impl(mgx_handle *h, const int32_t *actions_dev, int K,
                        h->lds_rollout, (hipStream_t)stream, h->kp, o, actions_dev, K)
     switch (var) {
         // S = 8 (configs 2, 3 and 4): the grid size a constant (render and grid-copy address math in immediates)
-        case 0: if (MGX_ROLL_S8 && h->kp.S == 8) MGX_ROLL(false, false, false, 8); else MGX_ROLL(false, false, false, 0); break;
-        case 1: if (MGX_ROLL_S8 && h->kp.S == 8) MGX_ROLL(false, false, true, 8); else MGX_ROLL(false, false, true, 0); break;
+        case 0: if (h->kp.S == 8) MGX_ROLL(false, false, false, 8); else MGX_ROLL(false, false, false, 0); break;
+        case 1: if (h->kp.S == 8) MGX_ROLL(false, false, true, 8); else MGX_ROLL(false, false, true, 0); break;
         case 2: MGX_ROLL(false, true, false); break;
         case 3: MGX_ROLL(false, true, true); break;
         case 4: MGX_ROLL(true, false, false); break;
@@ -3331,10 +3274,6 @@ static mgx_status rollout_impl(mgx_handle *h, const int32_t *actions_dev, int K,
     }
 #undef MGX_ROLL
     HIP_TRY(hipGetLastError());
-    if (fork && MGX_ROLLOUT_FIRST) {
-        mgx_status fs = fork_end(h);
-        if (fs != MGX_OK) return fs;
-    }
     h->calls += (uint64_t)K;
     if (o.gshard) {   // fold the launch's GAE partials into the caller's triple (as mgx_gae_dones)
         hipLaunchKernelGGL(mgx_gae_reduce_kernel, dim3(1), dim3(GAE_SHARDS), 0, (hipStream_t)stream,

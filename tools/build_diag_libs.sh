@@ -9,15 +9,11 @@ declare -A V=(
   [rstamps]="-DMGX_RSTAMPS=1"
   [rstamps_serial]="-DMGX_RSTAMPS=1 -DMGX_SERIAL_REFILL=1"
   [rclock]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1"
-  [nos8]="-DMGX_ROLL_S8=0"
-  [nostep8]="-DMGX_STEP_S8=0"
   [skip1]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=1"
   [skip2]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=2"
   [skip4]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=4"
   [skip8]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=8"
   [skip32]="-DMGX_REFILL_CLOCK=1 -DMGX_SERIAL_REFILL=1 -DMGX_GEN_SKIP=32"
-  [nos8r]="-DMGX_REFILL_S8=0"
-  [rollfirst]="-DMGX_ROLLOUT_FIRST=1"
   [epw64]="-DMGX_REFILL_EPW=64"
   [epw32]="-DMGX_REFILL_EPW=32"
   [epw16]="-DMGX_REFILL_EPW=16"
@@ -25,19 +21,12 @@ declare -A V=(
   [prio1]="-DMGX_REFILL_PRIO=1"
   [prio0]="-DMGX_REFILL_PRIO=0"
   [vmsync]="-DMGX_ROLL_VMKEEP=-1"
-  [nodefer]="-DMGX_ROLL_DEFER_ROWS=0"
   [vm0]="-DMGX_ROLL_VMKEEP=0"
   [vm6]="-DMGX_ROLL_VMKEEP=6"
   [vm4]="-DMGX_ROLL_VMKEEP=4"
   [vm8]="-DMGX_ROLL_VMKEEP=8"
   [vm12]="-DMGX_ROLL_VMKEEP=12"
   [vm16]="-DMGX_ROLL_VMKEEP=16"
-  [topup4]="-DMGX_MT_TOPUP=4"
-  [topup2]="-DMGX_MT_TOPUP=2"
-  [r3rounds]="-DMGX_REFILL_ROUNDS=1"
-  [nos8r_serial]="-DMGX_REFILL_S8=0 -DMGX_SERIAL_REFILL=1"
-  [notok]="-DMGX_GEN_SKIP=64"
-  [popatomic]="-DMGX_ROLL_POPCNT=0"
   [wg16_serial]="-DMGX_MT_WG1=16 -DMGX_SERIAL_REFILL=1"
   [relaxed]="-DMGX_PUBN_ACQUIRE=0"
   [lprio3]="-DMGX_ROLL_LOGIC_PRIO=3"
