@@ -1517,50 +1517,58 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             RSTAMP(4);                                     // rows out + the block barrier
         }
         if (K > 0) rows_out_block(K - 1, tid, BLOCK_THREADS);   // the last step's rows
-        if (o.gadv && wave0) {
-            // mgx_rollout_compact_gae: mgx_gae_kernel<true>'s recurrence (same fp32 op order) for this lane's
-            // env over the K steps it just ran, from the rewards / dones it wrote itself (program order), eight
-            // steps' loads in flight at a time
-            double s1 = 0.0, s2 = 0.0;
-            if (lane < ne) {
-                const int64_t col = e0 + lane;
-                float last = 0.0f, nv = o.glv[col];
-                for (int t0 = K - 1; t0 >= 0; t0 -= 8) {
-                    float rr[8], vv[8], dd[8];
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        const int t = t0 - i;
-                        const int64_t k = (int64_t)(t >= 0 ? t : 0) * N + col;
-                        rr[i] = o.reward[k];
-                        vv[i] = o.gv[k];
-                        dd[i] = (float)o.done[k];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        const int t = t0 - i;
-                        if (t < 0) break;
-                        const int64_t k = (int64_t)t * N + col;
-                        const float nnt = 1.0f - dd[i];
-                        const float delta = (rr[i] + (o.gg * nv) * nnt) - vv[i];
-                        last = delta + (o.gc * nnt) * last;
-                        o.gadv[k] = last;
-                        o.gret[k] = last + vv[i];
-                        s1 += (double)last;
-                        s2 += (double)last * (double)last;
-                        nv = vv[i];
-                    }
+    }
+    if (o.gadv) {
+        // mgx_rollout_compact_gae: mgx_gae_kernel<true>'s recurrence (same fp32 op order) for this workgroup's envs
+        // over the K steps it just ran.  Round 5: the rewards / dones it wrote and the caller's values are staged in
+        // LDS tiles of GAE_RT steps by all five waves -- one load round trip per tile -- in the frame-row area,
+        // free once the last rows are out; wave 0 then runs the recurrence from LDS (round 4: wave 0 alone read
+        // them back in dependent batches of 8 steps, ~15 us on the launch's tail).
+        constexpr int GAE_RT = 16;                       // [16][64] f32 r, f32 v, u8 d = 9,216 B <= the 9,472-B rows
+        static_assert(GAE_RT * BLOCK_ENVS * 9 <= ((BLOCK_ENVS * FROW + 15) & ~15), "GAE tile in the frame rows");
+        float *g_r = reinterpret_cast<float *>(s_stk), *g_v = g_r + GAE_RT * BLOCK_ENVS;
+        uint8_t *g_d = reinterpret_cast<uint8_t *>(g_v + GAE_RT * BLOCK_ENVS);
+        __syncthreads();                                 // the last rows' copy-out has read s_stk
+        const bool act = wave0 && lane < ne;
+        float last = 0.0f, nv = act ? o.glv[e0 + lane] : 0.0f;
+        double s1 = 0.0, s2 = 0.0;
+        for (int thi = K - 1; thi >= 0; thi -= GAE_RT) {
+            const int nt = min(GAE_RT, thi + 1);
+            for (int idx = tid; idx < nt * BLOCK_ENVS; idx += ROLL_THREADS) {
+                const int i = idx >> 6, l = idx & (BLOCK_ENVS - 1);
+                if (l < ne) {
+                    const int64_t k = (int64_t)(thi - i) * N + e0 + l;
+                    g_r[idx] = o.reward[k];
+                    g_v[idx] = o.gv[k];
+                    g_d[idx] = o.done[k];
                 }
             }
-            if (o.gshard) {
-                for (int off = 32; off > 0; off >>= 1) {
-                    s1 += __shfl_down(s1, off);
-                    s2 += __shfl_down(s2, off);
+            __syncthreads();
+            if (act) {
+                for (int i = 0; i < nt; i++) {
+                    const int64_t k = (int64_t)(thi - i) * N + e0 + lane;
+                    const float rr = g_r[i * BLOCK_ENVS + lane], vv = g_v[i * BLOCK_ENVS + lane];
+                    const float nnt = 1.0f - (float)g_d[i * BLOCK_ENVS + lane];
+                    const float delta = (rr + (o.gg * nv) * nnt) - vv;
+                    last = delta + (o.gc * nnt) * last;
+                    o.gadv[k] = last;
+                    o.gret[k] = last + vv;
+                    s1 += (double)last;
+                    s2 += (double)last * (double)last;
+                    nv = vv;
                 }
-                if (lane == 0) {
-                    double *sh = o.gshard + 2 * (blockIdx.x & 255);   // GAE_SHARDS slots, as mgx_gae_kernel
-                    atomicAdd(&sh[0], s1);
-                    atomicAdd(&sh[1], s2);
-                }
+            }
+            __syncthreads();                             // wave 0 has read the tile before the next one lands
+        }
+        if (o.gshard && wave0) {
+            for (int off = 32; off > 0; off >>= 1) {
+                s1 += __shfl_down(s1, off);
+                s2 += __shfl_down(s2, off);
+            }
+            if (lane == 0) {
+                double *sh = o.gshard + 2 * (blockIdx.x & 255);   // GAE_SHARDS slots, as mgx_gae_kernel
+                atomicAdd(&sh[0], s1);
+                atomicAdd(&sh[1], s2);
             }
         }
     }
