@@ -46,12 +46,16 @@
 #ifndef MGX_REFILL_EPW       // envs per S = 8 refill wave: 0 auto (32 when 64-env waves leave SIMDs idle), 16, 32, 64
 #define MGX_REFILL_EPW 0
 #endif
+#ifndef MGX_ROLL_EPB_S16     // envs per fused-rollout block at S = 16 (config 5): 64, or 32 (twice the blocks, half the LDS)
+#define MGX_ROLL_EPB_S16 64
+#endif
 #ifndef MGX_ROLL_LOGIC_PRIO  // fused rollout: s_setprio of wave 0 during its step logic (0: none; the block waits for it)
 #define MGX_ROLL_LOGIC_PRIO 0
 #endif
-#ifndef MGX_SLIDE_FENCE      // 1: the MT slide orders its reductions with __threadfence() (an L2 write-back per workgroup;
-#define MGX_SLIDE_FENCE 0    // round 4), 0: by waiting for its returning atomics
-#endif
+#ifndef MGX_SLIDE_FENCE      // 1: the MT slide orders its reductions with __threadfence() (an L2 write-back per workgroup),
+#define MGX_SLIDE_FENCE 1    // 0: by waiting for its returning atomics.  Round 5 A/B (rotating order, 3 + 2 rounds): the
+#endif                      // fenced slide is the faster pipeline -- 20-step line 5.88 vs 5.71, default line 7.97-8.07 vs 7.35
+                            // x 10^9 (its write-back also cleans the L2 the next refill works in); kept
 #ifndef MGX_PUBN_ACQUIRE     // 1: the fused rollout reads ring_pubn with an agent-scope acquire (0: relaxed; A/B of the
 #define MGX_PUBN_ACQUIRE 1   // acquire's cost)
 #endif

@@ -491,7 +491,8 @@ __device__ __forceinline__ void sync_keep_vm() {
 // =============================================================== step kernel
 // Grids in the step kernel's LDS are chunk-major, [GS/16][64 lanes][16 B] (the LDS-DMA
 // layout: one 16-B chunk per lane per global_load_lds); byte b of lane le's grid:
-__device__ __forceinline__ int cm_off(int le, int b) { return (b >> 4) * (BLOCK_ENVS * 16) + le * 16 + (b & 15); }
+template <int EPB = BLOCK_ENVS>   // envs per block (the chunk stride; the fused rollout also runs 32-env blocks)
+__device__ __forceinline__ int cm_off(int le, int b) { return (b >> 4) * (EPB * 16) + le * 16 + (b & 15); }
 
 // Render the view columns thread q (0..3) of env slot `le` owns -- vx = q and q + 4; thread 3
 // only column 3, which holds the agent's own cell (3, 6) -- into a frame row fr ([type 49]
@@ -504,6 +505,7 @@ __device__ __forceinline__ int cm_off(int le, int b) { return (b >> 4) * (BLOCK_
 // Along a column the world cell moves by -dir_vec per vy (adds only, no multiplies).  `grids`
 // is the block's current grids or its popped episodes' grids (both chunk-major).  Every grid
 // byte is read before any frame byte is written: one LDS round trip.
+template <int EPB = BLOCK_ENVS>
 __device__ __forceinline__ void render_cols(const uint8_t *grids, int S, int le, int q, uint32_t rp, uint8_t *fr) {
     const int ax = rp & 0xFF, ay = (rp >> 8) & 0xFF, dir = (rp >> 16) & 3;
     const uint8_t carry = (uint8_t)(rp >> 24);
@@ -518,7 +520,7 @@ __device__ __forceinline__ void render_cols(const uint8_t *grids, int S, int le,
         for (int vy = 0; vy < 7; vy++) {
             const uint32_t cx = min((uint32_t)wx, (uint32_t)(S - 1)), cy = min((uint32_t)wy, (uint32_t)(S - 1));
             const int b = (int)__umul24(cy, (uint32_t)S) + (int)cx;
-            code[j][vy] = base[b + __mul24(b >> 4, BLOCK_ENVS * 16 - 16)];   // cm_off(le, b)
+            code[j][vy] = base[b + __mul24(b >> 4, EPB * 16 - 16)];   // cm_off<EPB>(le, b)
             wx -= dx;
             wy -= dy;
         }
@@ -550,6 +552,7 @@ struct StepRes {
     uint8_t carry;                    // carried object after the key consumption (Q4)
     bool term, trunc, done, dirty;    // dirty: the grid changed
 };
+template <int EPB = BLOCK_ENVS>
 __device__ __forceinline__ StepRes env_step(const EnvState &st, int a, uint8_t *grids, int le, int S, int manual,
                                             uint64_t mrange) {
     StepRes R;
@@ -558,7 +561,7 @@ __device__ __forceinline__ StepRes env_step(const EnvState &st, int a, uint8_t *
     int ax = st.ax, ay = st.ay, dir = st.dir;
     uint8_t carry = st.carry;
     const int fx = ax + ((dir == 0) - (dir == 2)), fy = ay + ((dir == 1) - (dir == 3));
-    uint8_t *fp = grids + cm_off(le, fy * S + fx);
+    uint8_t *fp = grids + cm_off<EPB>(le, fy * S + fx);
     const uint8_t fc = *fp;
     const int ft = fc & 15;
     // MiniGridEnv.step (3P)
@@ -1214,48 +1217,53 @@ constexpr int ROLL_THREADS = BLOCK_THREADS + 64;
 // step): VIS see_through_walls == False (Grid.process_vis), MOVE 'move' missions (problems mov / full: target
 // ranges), R64 the optional f64 rewards.  ep_return / ep_len / livelock (after the last step only) are kept in
 // LDS and written after the loop.
-template <bool VIS, bool MOVE, bool R64, int SC = 0>   // SC > 0: the grid size as a compile-time constant
-__global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p, ROut o, const int32_t *__restrict__ actions,
+// EPB: envs per block, 64 or 32 (round 5, S = 16: config 5's 63-KB workgroups fitted two to a CU; at 32 envs the
+// same LDS per env, twice as many workgroups): 4 * EPB render threads (wave 0 also runs the step logic, lanes
+// >= EPB idle) + the DMA wave.
+template <bool VIS, bool MOVE, bool R64, int SC = 0, int EPB = BLOCK_ENVS>   // SC > 0: the grid size as a constant
+__global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p, ROut o, const int32_t *__restrict__ actions,
                                                                       int K) {
+    static_assert(EPB == 64 || EPB == 32, "envs per block");
+    constexpr int RT = 4 * EPB, RTH = RT + 64;       // render threads, all threads
     extern __shared__ __align__(16) uint8_t smem[];
-    constexpr int CSTK = (BLOCK_ENVS * FROW + 15) & ~15;
-    const int GSQ = SC > 0 ? ((SC * SC + 15) & ~15) >> 4 : p.GS >> 4, GB = GSQ * BLOCK_ENVS * 16;
+    constexpr int CSTK = (EPB * FROW + 15) & ~15;
+    const int GSQ = SC > 0 ? ((SC * SC + 15) & ~15) >> 4 : p.GS >> 4, GB = GSQ * EPB * 16;
     uint8_t *s_stk = smem;                                             // frame rows [64][148]
     uint8_t *s_grid = smem + CSTK;                                     // current grids (chunk-major, cm_off)
     uint8_t *s_pg = s_grid + GB;                                       // [2] staged ring episodes' grids
     uint4 *s_ph = reinterpret_cast<uint4 *>(s_pg + 2 * GB);            // [2][64] their headers
-    int32_t *s_act = reinterpret_cast<int32_t *>(s_ph + 2 * BLOCK_ENVS);   // [2][64] actions
-    unsigned long long *s_mr = reinterpret_cast<unsigned long long *>(s_act + 2 * BLOCK_ENVS);
+    int32_t *s_act = reinterpret_cast<int32_t *>(s_ph + 2 * EPB);   // [2][64] actions
+    unsigned long long *s_mr = reinterpret_cast<unsigned long long *>(s_act + 2 * EPB);
                                                                        // [64] 'move' target_range (has_move only)
-    __shared__ uint32_t s_rp[BLOCK_ENVS];        // render params of the frame written (post-step view or
+    __shared__ uint32_t s_rp[EPB];        // render params of the frame written (post-step view or
                                                  // the popped episode's first)
-    __shared__ uint32_t s_rpt[BLOCK_ENVS];       // post-step view of a finished episode (terminal row)
-    __shared__ uint8_t s_term[BLOCK_ENVS];       // terminal row written this step
-    __shared__ uint8_t s_popb[BLOCK_ENVS];       // staged buffer popped this step (0xFF: none)
+    __shared__ uint32_t s_rpt[EPB];       // post-step view of a finished episode (terminal row)
+    __shared__ uint8_t s_term[EPB];       // terminal row written this step
+    __shared__ uint8_t s_popb[EPB];       // staged buffer popped this step (0xFF: none)
     // [step & 1] new ring head of an env that popped; NO_POP: none (u32: every rpos_t value is a real one)
-    __shared__ uint32_t s_nh[2][BLOCK_ENVS];
+    __shared__ uint32_t s_nh[2][EPB];
     __shared__ unsigned long long s_tmask;
     // per-env state between steps lives in LDS, not registers: a loop-carried value would stay live
     // through the render, where the register pressure peaks (in registers: 128 VGPRs, 3 workgroups
     // per CU instead of 4)
-    __shared__ uint4 s_st[BLOCK_ENVS];           // EnvState
-    __shared__ rpos_t s_head[BLOCK_ENVS], s_pub[BLOCK_ENVS];
+    __shared__ uint4 s_st[EPB];           // EnvState
+    __shared__ rpos_t s_head[EPB], s_pub[EPB];
     __shared__ unsigned long long s_cnt[2];      // resets, abandoned attempts
     __shared__ uint32_t s_err;
-    __shared__ float s_lrew[BLOCK_ENVS];         // the last step's reward, step count, abandoned attempts
-    __shared__ int s_lsc[BLOCK_ENVS], s_lll[BLOCK_ENVS];
+    __shared__ float s_lrew[EPB];         // the last step's reward, step count, abandoned attempts
+    __shared__ int s_lsc[EPB], s_lll[EPB];
 
-    const int tid = threadIdx.x, lane = tid & (BLOCK_ENVS - 1);
-    const int64_t e0 = (int64_t)blockIdx.x * BLOCK_ENVS;
+    const int tid = threadIdx.x, lane = tid & 63;     // (wave 0 and the DMA wave: env = lane, lanes >= EPB idle)
+    const int64_t e0 = (int64_t)blockIdx.x * EPB;
     const int64_t N = p.n;
-    const int ne = (int)min<int64_t>(BLOCK_ENVS, N - e0);
+    const int ne = (int)min<int64_t>(EPB, N - e0);
     const int S = SC > 0 ? SC : p.S, D = p.D;
-    const bool wave0 = tid < BLOCK_ENVS, dmaw = tid >= BLOCK_THREADS;
+    const bool wave0 = tid < 64, dmaw = tid >= RT;
     const int lc = min(lane, ne - 1);
     __shared__ unsigned long long s_t0;           // kernel clock: this workgroup's start
     if (p.clk.slots && tid == 0) s_t0 = clk_now();
     // ---- setup: ring positions and state (waves 0 and 4), grids (waves 0-3, LDS-DMA)
-    if (wave0) {
+    if (wave0 && lane < EPB) {
         s_st[lane] = reinterpret_cast<const uint4 *>(p.state)[e0 + lc];
         s_head[lane] = p.ring_head[e0 + lc];
         if (MOVE) s_mr[lane] = p.range_cur[e0 + lc];
@@ -1263,10 +1271,10 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         if (lane < 2) s_cnt[lane] = 0;
         if (lane == 0) s_err = 0;
     }
-    if (!dmaw) {
+    if (!dmaw && lane < EPB) {                       // (LDS-DMA: lane l writes chunk byte l * 16)
         const uint4 *src = reinterpret_cast<const uint4 *>(p.grid + (e0 + lc) * p.GS);
-        for (int c = tid >> 6; c < GSQ; c += BLOCK_THREADS / 64)
-            __builtin_amdgcn_global_load_lds(src + c, s_grid + c * (BLOCK_ENVS * 16), 16, 0, 0);
+        for (int c = tid >> 6; c < GSQ; c += RT / 64)
+            __builtin_amdgcn_global_load_lds(src + c, s_grid + c * (EPB * 16), 16, 0, 0);
     }
     // stage ring episode h of env e (this lane's) into buffer h & 1: header, grid
     auto stage = [&](rpos_t h) {
@@ -1284,12 +1292,12 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         const uint32_t par = h & 1;
         if (par == 0) {
             __builtin_amdgcn_global_load_lds(hs, s_ph, 16, 0, 0);
-            for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + c * (BLOCK_ENVS * 16), 16, 0, 0);
+            for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + c * (EPB * 16), 16, 0, 0);
             asm volatile("" ::: "memory");
         }
         if (par != 0) {
-            __builtin_amdgcn_global_load_lds(hs, s_ph + BLOCK_ENVS, 16, 0, 0);
-            for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + GB + c * (BLOCK_ENVS * 16), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(hs, s_ph + EPB, 16, 0, 0);
+            for (int c = 0; c < GSQ; c++) __builtin_amdgcn_global_load_lds(gs + c, s_pg + GB + c * (EPB * 16), 16, 0, 0);
             asm volatile("" ::: "memory");
         }
     };
@@ -1334,13 +1342,13 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             const int tb = t & 1;
             int tidv = tid;
             asm volatile("" : "+v"(tidv));
-            const int lanev = tidv & (BLOCK_ENVS - 1);
+            const int lanev = tidv & 63;
             // the next step's actions; the ring episode after next of every env that popped last step
             // (LDS-DMA only: a register load here would make the wave wait for it -- and for every
             // prefetch in flight -- before the post-logic barrier, the whole block with it)
             if (lanev < ne) {
                 if (t + 1 < K)
-                    __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lanev, s_act + (tb ^ 1) * BLOCK_ENVS,
+                    __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lanev, s_act + (tb ^ 1) * EPB,
                                                      4, 0, 0);
                 const uint32_t nh = s_nh[tb ^ 1][lanev];
                 if (nh != NO_POP && (rpos_t)(s_pub[lanev] - nh) > 1) stage((rpos_t)(nh + 1));
@@ -1380,14 +1388,14 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             if (t > 0 && !wave0) {
                 int tq = tid;
                 asm volatile("" : "+v"(tq));
-                rows_out_block(t - 1, tq - BLOCK_ENVS, BLOCK_THREADS - BLOCK_ENVS);
+                rows_out_block(t - 1, tq - 64, RT - 64);
             }
             // thread index through an opaque copy: lane- / env-derived addresses are then computed inside
             // each region of the step, instead of being hoisted out of the loop and kept live through all of
             // them (96 -> fewer VGPRs; the render's and the step logic's registers no longer add up)
             int tidv = tid;
             asm volatile("" : "+v"(tidv));
-            const int lanev = tidv & (BLOCK_ENVS - 1);
+            const int lanev = tidv & 63;
             if (wave0) {
                 // ---- the step: one lanev per env.  The block waits for this one wave at the post-logic barrier:
                 // MGX_ROLL_LOGIC_PRIO raises its issue priority for the phase (over the co-resident refill waves'
@@ -1408,9 +1416,9 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                     rpos_t rhead = s_head[lanev];
                     uint64_t mrange = MOVE ? s_mr[lanev] : 0ull;
                     uint32_t err = 0;
-                    int a = s_act[tb * BLOCK_ENVS + lanev];
+                    int a = s_act[tb * EPB + lanev];
                     if ((unsigned)a > 6u) { err |= MGX_DEVERR_BAD_ACTION; a = -1; }
-                    const StepRes r = env_step(st, a, s_grid, lanev, S, p.manual, mrange);
+                    const StepRes r = env_step<EPB>(st, a, s_grid, lanev, S, p.manual, mrange);
                     tw = r.done && (p.terminal_mode == MGX_TERMINAL_ALL ||
                                     (p.terminal_mode == MGX_TERMINAL_TRUNCATED && r.trunc && !r.term));
                     s_rpt[lanev] = r.view;
@@ -1428,7 +1436,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                     if (r.done && (rpos_t)(s_pub[lanev] - rhead) != 0) {
                         // SubprocVecEnv auto-reset: the staged ring episode (header, RNG snapshot, grid)
                         popb = rhead & 1;
-                        const uint4 h = s_ph[popb * BLOCK_ENVS + lanev];
+                        const uint4 h = s_ph[popb * EPB + lanev];
                         if (MOVE) s_mr[lanev] = p.ring_range[e * (uint32_t)D + (rhead & (D - 1))];
                         mid = (uint8_t)(h.y >> 16);
                         st.ax = (uint8_t)(h.x & 0xFF); st.ay = (uint8_t)((h.x >> 8) & 0xFF); st.dir = (uint8_t)((h.x >> 16) & 0xFF);
@@ -1457,9 +1465,11 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                     }
                     if (err) atomicOr(&s_err, err);
                 }
-                s_term[lanev] = tw;
-                s_popb[lanev] = popb;
-                s_nh[tb][lanev] = nh;
+                if (lanev < EPB) {
+                    s_term[lanev] = tw;
+                    s_popb[lanev] = popb;
+                    s_nh[tb][lanev] = nh;
+                }
                 const unsigned long long tm = __ballot(tw);
                 // resets: one popcount of the wave's pops, added by lane 0 (only wave 0 writes s_cnt), instead of
                 // a 64-bit LDS atomic per popping lane on one address (round 4)
@@ -1478,7 +1488,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             if (s_tmask) {
                 // terminal rows (rare, block-uniform): the finished episode's last view, rendered into the
                 // env's frame row from its post-step grid and copied out before the row is reused below
-                if (le < ne && s_term[le]) render_cols(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW + 1);
+                if (le < ne && s_term[le]) render_cols<EPB>(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW + 1);
                 __syncthreads();
                 if (VIS) {
                     if (tidv < ne && s_term[tidv]) apply_vis(s_stk + tidv * FROW + 1);
@@ -1500,12 +1510,12 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
                 const uint8_t b = s_popb[le];
                 const uint8_t *g = b == 0xFF ? s_grid : s_pg + b * GB;
                 const uint32_t rp = s_rp[le];
-                render_cols(g, S, le, q, rp, s_stk + le * FROW + 1);
+                render_cols<EPB>(g, S, le, q, rp, s_stk + le * FROW + 1);
                 if (q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);
                 if (b != 0xFF)
                     for (int c = q; c < GSQ; c += 4)
-                        *reinterpret_cast<uint4 *>(s_grid + c * (BLOCK_ENVS * 16) + le * 16) =
-                            *reinterpret_cast<const uint4 *>(g + c * (BLOCK_ENVS * 16) + le * 16);
+                        *reinterpret_cast<uint4 *>(s_grid + c * (EPB * 16) + le * 16) =
+                            *reinterpret_cast<const uint4 *>(g + c * (EPB * 16) + le * 16);
             }
             if (VIS) {
                 __syncthreads();
@@ -1516,7 +1526,7 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             sync_keep_vm<MGX_ROLL_VMKEEP>();               // B
             RSTAMP(4);                                     // rows out + the block barrier
         }
-        if (K > 0) rows_out_block(K - 1, tid, BLOCK_THREADS);   // the last step's rows
+        if (K > 0) rows_out_block(K - 1, tid, RT);   // the last step's rows
     }
     if (o.gadv) {
         // mgx_rollout_compact_gae: mgx_gae_kernel<true>'s recurrence (same fp32 op order) for this workgroup's envs
@@ -1525,17 +1535,17 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
         // free once the last rows are out; wave 0 then runs the recurrence from LDS (round 4: wave 0 alone read
         // them back in dependent batches of 8 steps, ~15 us on the launch's tail).
         constexpr int GAE_RT = 16;                       // [16][64] f32 r, f32 v, u8 d = 9,216 B <= the 9,472-B rows
-        static_assert(GAE_RT * BLOCK_ENVS * 9 <= ((BLOCK_ENVS * FROW + 15) & ~15), "GAE tile in the frame rows");
-        float *g_r = reinterpret_cast<float *>(s_stk), *g_v = g_r + GAE_RT * BLOCK_ENVS;
-        uint8_t *g_d = reinterpret_cast<uint8_t *>(g_v + GAE_RT * BLOCK_ENVS);
+        static_assert(GAE_RT * EPB * 9 <= ((EPB * FROW + 15) & ~15), "GAE tile in the frame rows");
+        float *g_r = reinterpret_cast<float *>(s_stk), *g_v = g_r + GAE_RT * EPB;
+        uint8_t *g_d = reinterpret_cast<uint8_t *>(g_v + GAE_RT * EPB);
         __syncthreads();                                 // the last rows' copy-out has read s_stk
         const bool act = wave0 && lane < ne;
         float last = 0.0f, nv = act ? o.glv[e0 + lane] : 0.0f;
         double s1 = 0.0, s2 = 0.0;
         for (int thi = K - 1; thi >= 0; thi -= GAE_RT) {
             const int nt = min(GAE_RT, thi + 1);
-            for (int idx = tid; idx < nt * BLOCK_ENVS; idx += ROLL_THREADS) {
-                const int i = idx >> 6, l = idx & (BLOCK_ENVS - 1);
+            for (int idx = tid; idx < nt * EPB; idx += RTH) {
+                const int i = idx / EPB, l = idx & (EPB - 1);
                 if (l < ne) {
                     const int64_t k = (int64_t)(thi - i) * N + e0 + l;
                     g_r[idx] = o.reward[k];
@@ -1547,8 +1557,8 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
             if (act) {
                 for (int i = 0; i < nt; i++) {
                     const int64_t k = (int64_t)(thi - i) * N + e0 + lane;
-                    const float rr = g_r[i * BLOCK_ENVS + lane], vv = g_v[i * BLOCK_ENVS + lane];
-                    const float nnt = 1.0f - (float)g_d[i * BLOCK_ENVS + lane];
+                    const float rr = g_r[i * EPB + lane], vv = g_v[i * EPB + lane];
+                    const float nnt = 1.0f - (float)g_d[i * EPB + lane];
                     const float delta = (rr + (o.gg * nv) * nnt) - vv;
                     last = delta + (o.gc * nnt) * last;
                     o.gadv[k] = last;
@@ -1611,15 +1621,16 @@ __global__ __launch_bounds__(ROLL_THREADS, 4) void mgx_rollout_kernel(KParams p,
     }
     if (!dmaw) {
         uint4 *dst = reinterpret_cast<uint4 *>(p.grid + e0 * p.GS);
-        for (int i = tid; i < ne * GSQ; i += BLOCK_THREADS) {
+        for (int i = tid; i < ne * GSQ; i += RT) {
             const int le = i / GSQ, c = i - le * GSQ;
-            dst[i] = *reinterpret_cast<const uint4 *>(s_grid + c * (BLOCK_ENVS * 16) + le * 16);
+            dst[i] = *reinterpret_cast<const uint4 *>(s_grid + c * (EPB * 16) + le * 16);
         }
     }
     if (tid == 0) {
-        atomicAdd(&p.blk[blockIdx.x].x, (unsigned long long)ne * (unsigned long long)K);
-        if (s_cnt[0]) atomicAdd(&p.blk[blockIdx.x].y, s_cnt[0]);
-        if (s_cnt[1]) atomicAdd(&p.blk[blockIdx.x].z, s_cnt[1]);
+        const int sb = (int)(blockIdx.x / (64 / EPB));   // the stats slot of these 64 envs (32-env blocks: two)
+        atomicAdd(&p.blk[sb].x, (unsigned long long)ne * (unsigned long long)K);
+        if (s_cnt[0]) atomicAdd(&p.blk[sb].y, s_cnt[0]);
+        if (s_cnt[1]) atomicAdd(&p.blk[sb].z, s_cnt[1]);
         if (s_err) atomicOr(p.err, s_err);
     }
     if (p.clk.slots) {                            // every wave of the workgroup is done
@@ -2040,11 +2051,12 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
             mn = s_red[w] < mn ? s_red[w] : mn;
             mx = s_red2[w] > mx ? s_red2[w] : mx;
         }
-        // Returning atomics, waited for: each has been performed at the device-scope coherence point when its
-        // value is back, which orders it before this workgroup's done-counter increment (round 5: with
-        // __threadfence() instead, every workgroup and the last one wrote back their XCD's whole L2 --
-        // buffer_wbl2 -- which the co-resident rollout keeps full of dirty row lines).  Everything the last
-        // workgroup reads of this pass it reads with atomics; MtCtl's plain fields come from earlier kernels.
+        // The reductions are ordered before this workgroup's done-counter increment either by __threadfence()
+        // (MGX_SLIDE_FENCE, the product: every workgroup and the last one write back their XCD's L2 -- buffer_wbl2)
+        // or by waiting for the returning atomics (each has been performed at the device-scope coherence point when
+        // its value is back; everything the last workgroup reads of this pass it reads with atomics, MtCtl's plain
+        // fields come from earlier kernels).  Round 5 A/B: the fenced slide is the faster PIPELINE (the next refill
+        // runs ~5-10 % faster after the write-back), although the fence-free slide itself is shorter.
         const unsigned long long r0 = atomicMin(&c->span_min, mn);
         const unsigned long long r1 = atomicMax(&c->span_max, mx);
         const unsigned long long r2 = cs ? atomicAdd(&c->cons_run, cs) : 0ull;   // (wave 0 holds this workgroup's blocks)
@@ -2527,7 +2539,8 @@ struct mgx_handle {
     mgx_config cfg;
     int device;
     KParams kp;
-    size_t lds_step, lds_step_compact, lds_reset, lds_refill, lds_rollout;
+    size_t lds_step, lds_step_compact, lds_reset, lds_refill, lds_rollout, lds_rollout32;
+    int roll_epb;           // envs per fused-rollout block: 64, or 32 at S = 16 (MGX_ROLL_EPB_S16)
     int nw;                 // 64-bit words of the generator's S*S cell masks (1, 2 or 4)
     bool ext;               // generator variant with full / drp / mov / obstacles
     int refill_every;       // K: steps per refill epoch
@@ -2848,9 +2861,13 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_step_kernel<int64_t, true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_step_compact));
     // fused rollout: frame rows + current grids + two staged ring episodes (grid, header) + actions
     // [+ 'move' target ranges]
-    h->lds_rollout = (size_t)((BLOCK_ENVS * FROW + 15) & ~15) + (size_t)BLOCK_ENVS * 3 * GS +
-                     (size_t)BLOCK_ENVS * 2 * 16 + (size_t)2 * BLOCK_ENVS * 4 +
-                     ((cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL) ? (size_t)BLOCK_ENVS * 8 : 0);
+    const auto roll_lds = [&](int epb) {
+        return (size_t)((epb * FROW + 15) & ~15) + (size_t)epb * 3 * GS + (size_t)epb * 2 * 16 + (size_t)2 * epb * 4 +
+               ((cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL) ? (size_t)epb * 8 : 0);
+    };
+    h->lds_rollout = roll_lds(64);
+    h->lds_rollout32 = roll_lds(32);
+    h->roll_epb = (S == 16 && MGX_ROLL_EPB_S16 == 32) ? 32 : 64;
 #define MGX_ROLL_LDS(V, M, R)                                                                                     \
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<V, M, R>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 (int)h->lds_rollout))
@@ -2861,6 +2878,10 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
     HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<false, false, true, 8>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<false, false, false, 16, 32>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout32));
+    HIP_TRY(hipFuncSetAttribute((const void *)mgx_rollout_kernel<false, false, true, 16, 32>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_rollout32));
 #undef MGX_ROLL_LDS
     h->nw = S * S <= 64 ? 1 : (S * S <= 128 ? 2 : 4);
     h->ext = cfg->obstacles || cfg->problem == MGX_PROBLEM_FULL || cfg->problem == MGX_PROBLEM_DRP ||
@@ -3082,7 +3103,7 @@ mgx_status mgx_set_seed(mgx_handle *h, int64_t seed) {
 // grid of every launch of a clocked kernel class (the clock's per-workgroup records need one grid per class)
 static int clock_groups(const mgx_handle *h, int cls) {
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
-    if (cls == CLK_STEP) return (int)nblk;
+    if (cls == CLK_STEP) return (int)std::max<int64_t>(nblk, (h->kp.n + h->roll_epb - 1) / h->roll_epb);
     if (cls == CLK_SLIDE) return (int)((h->kp.n + SLIDE_ENVS - 1) / SLIDE_ENVS);
     return (int)((h->kp.n + h->kp.refill_epw - 1) / h->kp.refill_epw);   // (64 except the S = 8 kernel's 32/16)
 }
@@ -3269,10 +3290,23 @@ static mgx_status rollout_impl(mgx_handle *h, const int32_t *actions_dev, int K,
 #define MGX_ROLL(V, M, R, ...)                                                                                    \
     hipLaunchKernelGGL((mgx_rollout_kernel<V, M, R, ##__VA_ARGS__>), dim3((unsigned)nblk), dim3(ROLL_THREADS),   \
                        h->lds_rollout, (hipStream_t)stream, h->kp, o, actions_dev, K)
+    // S = 16 (config 5) with 32-env blocks: grid and LDS of their own
+#define MGX_ROLL32(R)                                                                                              \
+    hipLaunchKernelGGL((mgx_rollout_kernel<false, false, R, 16, 32>), dim3((unsigned)((h->kp.n + 31) / 32)),         \
+                       dim3(4 * 32 + 64), h->lds_rollout32, (hipStream_t)stream, h->kp, o, actions_dev, K)
+    const bool r32 = h->roll_epb == 32 && h->kp.S == 16;
     switch (var) {
         // S = 8 (configs 2, 3 and 4): the grid size a constant (render and grid-copy address math in immediates)
-        case 0: if (h->kp.S == 8) MGX_ROLL(false, false, false, 8); else MGX_ROLL(false, false, false, 0); break;
-        case 1: if (h->kp.S == 8) MGX_ROLL(false, false, true, 8); else MGX_ROLL(false, false, true, 0); break;
+        case 0:
+            if (h->kp.S == 8) MGX_ROLL(false, false, false, 8);
+            else if (r32) MGX_ROLL32(false);
+            else MGX_ROLL(false, false, false, 0);
+            break;
+        case 1:
+            if (h->kp.S == 8) MGX_ROLL(false, false, true, 8);
+            else if (r32) MGX_ROLL32(true);
+            else MGX_ROLL(false, false, true, 0);
+            break;
         case 2: MGX_ROLL(false, true, false); break;
         case 3: MGX_ROLL(false, true, true); break;
         case 4: MGX_ROLL(true, false, false); break;
@@ -3281,6 +3315,7 @@ static mgx_status rollout_impl(mgx_handle *h, const int32_t *actions_dev, int K,
         default: MGX_ROLL(true, true, true); break;
     }
 #undef MGX_ROLL
+#undef MGX_ROLL32
     HIP_TRY(hipGetLastError());
     h->calls += (uint64_t)K;
     if (o.gshard) {   // fold the launch's GAE partials into the caller's triple (as mgx_gae_dones)

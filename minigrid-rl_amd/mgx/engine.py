@@ -190,7 +190,9 @@ class MgxEngine:
         if last <= first:
             return []
         rec = self.clock[off + g:off + g * (1 + 2 * self.clock_slots)].view(self.clock_slots, g, 2)[first:last]
-        span = rec[:, :, 1].max(1).values - rec[:, :, 0].min(1).values       # (ticks < 2^63: signed is fine)
+        # (a launch with a smaller grid than the class's largest leaves its other records zero: not a start)
+        start = torch.where(rec[:, :, 0] > 0, rec[:, :, 0], torch.iinfo(torch.int64).max).min(1).values
+        span = rec[:, :, 1].max(1).values - start                               # (ticks < 2^63: signed is fine)
         return [float(x) * 1e3 / self.clock_khz for x in span.cpu().tolist()]
 
     def join(self):

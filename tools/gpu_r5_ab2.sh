@@ -12,6 +12,6 @@ tail -2 gpurun_out/ab2_tests.log
 K20="--steps 20 --warmup 5"
 L="- ab_libs/libmgx_lprio3.so ab_libs/libmgx_sfence.so ab_libs/libmgx_lp3sf.so ab_libs/libmgx_lp3sfrx.so"
 TAG=r5k20b ROUNDS=3 LIBS="$L" BENCH_ARGS="$K20" bash tools/gpu_ab.sh
-TAG=r5k20g ROUNDS=2 LIBS="$L" BENCH_ARGS="$K20 --gae-fused 1" bash tools/gpu_ab.sh
-TAG=r5defb ROUNDS=1 LIBS="$L" BENCH_ARGS="" bash tools/gpu_ab.sh
+TAG=r5k20g ROUNDS=2 LIBS="- ab_libs/libmgx_lp3sf.so" BENCH_ARGS="$K20 --gae-fused 1" bash tools/gpu_ab.sh
+TAG=r5defb ROUNDS=1 LIBS="- ab_libs/libmgx_lprio3.so ab_libs/libmgx_lp3sf.so" BENCH_ARGS="" bash tools/gpu_ab.sh
 echo done
