@@ -801,6 +801,13 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     int new_head = -1;
     bool done = false, term = false, trunc = false, dirty = false, fill = false, popped = false;
     int mdone = 0, rs = -1, dir = 0;
+    // the block waits for wave 0's logic at the next barrier: MGX_STEP_LOGIC_PRIO raises its issue priority for
+    // the phase (over the co-resident refill waves' 2), back to 0 after the ballot compaction below
+    if (MGX_STEP_LOGIC_PRIO && tid < BLOCK_ENVS) {
+        if (MGX_STEP_LOGIC_PRIO == 3) __builtin_amdgcn_s_setprio(3);
+        else if (MGX_STEP_LOGIC_PRIO == 2) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
+    }
     if (tid < ne) {
         const int64_t e = e0 + tid;
         if ((unsigned)a > 6u) { my_err |= MGX_DEVERR_BAD_ACTION; a = -1; }
@@ -885,6 +892,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
             s_nf = __popcll(fm); s_nd = __popcll(dm); s_npop = __popcll(pm); s_dmask = dm; s_tmask = tm;
             s_dirtym = gm;
         }
+        if (MGX_STEP_LOGIC_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     if (my_err) atomicOr(p.err, my_err);
     if (wave1) __builtin_amdgcn_s_waitcnt(0);          // the auto-reset prefetch has landed in LDS

@@ -33,6 +33,7 @@ declare -A V=(
   [lprio2]="-DMGX_ROLL_LOGIC_PRIO=2"
   [sfence]="-DMGX_SLIDE_FENCE=1"
   [epb32]="-DMGX_ROLL_EPB_S16=32"
+  [slprio3]="-DMGX_STEP_LOGIC_PRIO=3"
   [lp3sf]="-DMGX_ROLL_LOGIC_PRIO=3 -DMGX_SLIDE_FENCE=1"
   [lp3sfrx]="-DMGX_ROLL_LOGIC_PRIO=3 -DMGX_SLIDE_FENCE=1 -DMGX_PUBN_ACQUIRE=0"
 )
