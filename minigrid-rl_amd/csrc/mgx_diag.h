@@ -46,9 +46,9 @@
 #ifndef MGX_REFILL_EPW       // envs per S = 8 refill wave: 0 auto (32 when 64-env waves leave SIMDs idle), 16, 32, 64
 #define MGX_REFILL_EPW 0
 #endif
-#ifndef MGX_ROLL_EPB_S16     // envs per fused-rollout block at S = 16 (config 5): 64, or 32 (twice the blocks, half the LDS)
-#define MGX_ROLL_EPB_S16 64
-#endif
+#ifndef MGX_ROLL_EPB_S16     // envs per fused-rollout block at S = 16 (config 5): 64, or 32 (twice the blocks, half the LDS;
+#define MGX_ROLL_EPB_S16 32  // round 5 A/B, 2 rotating rounds: config 5 5.13-5.16 vs 5.05-5.06 x 10^9, kernel 24.4-24.6 vs
+#endif                      // 24.9 us per step)
 #ifndef MGX_ROLL_LOGIC_PRIO  // fused rollout: s_setprio of wave 0 during its step logic (0: none; the block waits for it)
 #define MGX_ROLL_LOGIC_PRIO 0
 #endif
