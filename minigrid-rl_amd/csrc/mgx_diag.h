@@ -56,9 +56,9 @@
 #define MGX_SLIDE_FENCE 1    // 0: by waiting for its returning atomics.  Round 5 A/B (rotating order, 3 + 2 rounds): the
 #endif                      // fenced slide is the faster pipeline -- 20-step line 5.88 vs 5.71, default line 7.97-8.07 vs 7.35
                             // x 10^9 (its write-back also cleans the L2 the next refill works in); kept
-#ifndef MGX_STEP_LOGIC_PRIO  // per-step kernel: s_setprio of wave 0 during its step logic (0: none)
-#define MGX_STEP_LOGIC_PRIO 0
-#endif
+#ifndef MGX_STEP_LOGIC_PRIO  // per-step kernel: s_setprio of wave 0 during its step logic (0: none).  Round 5 A/B (3
+#define MGX_STEP_LOGIC_PRIO 3  // rotating rounds, compact layout, 256 steps): 5.64-5.70 vs 5.46-5.47 x 10^9, kernel 7.6-7.7
+#endif                        // vs 8.1 us per step (the refill beside it 510 vs 450 us per epoch: it no longer bounds)
 #ifndef MGX_PUBN_ACQUIRE     // 1: the fused rollout reads ring_pubn with an agent-scope acquire (0: relaxed; A/B of the
 #define MGX_PUBN_ACQUIRE 1   // acquire's cost)
 #endif
