@@ -1390,6 +1390,7 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
             if (tt < rem)
                 reinterpret_cast<uint32_t *>(dst + nb16)[tt] = reinterpret_cast<const uint32_t *>(src + nb16)[tt];
         };
+        unsigned long long nres = 0;                 // wave 0: resets so far (ballot popcounts; s_cnt[0] after the loop)
         for (int t = 0; t < K; t++) {
             const int tb = t & 1;
             RSTAMP(0);
@@ -1425,6 +1426,11 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
                     uint64_t mrange = MOVE ? s_mr[lanev] : 0ull;
                     uint32_t err = 0;
                     int a = s_act[tb * EPB + lanev];
+                    // every LDS read the step may need, issued together with the state's (round 5): the published
+                    // end and BOTH staged headers (the popped buffer is rhead & 1, known only after s_head lands) --
+                    // the pop no longer waits on two more dependent LDS round trips after the step logic
+                    const rpos_t rpub = s_pub[lanev];
+                    const uint4 h0 = s_ph[lanev], h1 = s_ph[EPB + lanev];
                     if ((unsigned)a > 6u) { err |= MGX_DEVERR_BAD_ACTION; a = -1; }
                     const StepRes r = env_step<EPB>(st, a, s_grid, lanev, S, p.manual, mrange);
                     tw = r.done && (p.terminal_mode == MGX_TERMINAL_ALL ||
@@ -1441,10 +1447,10 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
                     }
                     uint8_t mid = st.mission_id;
                     int lvl = 0;
-                    if (r.done && (rpos_t)(s_pub[lanev] - rhead) != 0) {
+                    if (r.done && (rpos_t)(rpub - rhead) != 0) {
                         // SubprocVecEnv auto-reset: the staged ring episode (header, RNG snapshot, grid)
                         popb = rhead & 1;
-                        const uint4 h = s_ph[popb * EPB + lanev];
+                        const uint4 h = popb ? h1 : h0;
                         if (MOVE) s_mr[lanev] = p.ring_range[e * (uint32_t)D + (rhead & (D - 1))];
                         mid = (uint8_t)(h.y >> 16);
                         st.ax = (uint8_t)(h.x & 0xFF); st.ay = (uint8_t)((h.x >> 8) & 0xFF); st.dir = (uint8_t)((h.x >> 16) & 0xFF);
@@ -1482,10 +1488,8 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
                 // resets: one popcount of the wave's pops, added by lane 0 (only wave 0 writes s_cnt), instead of
                 // a 64-bit LDS atomic per popping lane on one address (round 4)
                 const unsigned long long pm = __ballot(popb != 0xFF);
-                if (lanev == 0) {
-                    s_tmask = tm;
-                    s_cnt[0] += (unsigned long long)__popcll(pm);
-                }
+                nres += (unsigned long long)__popcll(pm);   // (wave-uniform: a scalar register, written after the loop)
+                if (lanev == 0) s_tmask = tm;
                 if (MGX_ROLL_LOGIC_PRIO) __builtin_amdgcn_s_setprio(0);
             }
             RSTAMP(1);                                     // step logic (wave 0)
@@ -1535,6 +1539,7 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
             RSTAMP(4);                                     // rows out + the block barrier
         }
         if (K > 0) rows_out_block(K - 1, tid, RT);   // the last step's rows
+        if (wave0 && lane == 0) s_cnt[0] = nres;     // (read after the write-back section's barrier)
     }
     if (o.gadv) {
         // mgx_rollout_compact_gae: mgx_gae_kernel<true>'s recurrence (same fp32 op order) for this workgroup's envs
