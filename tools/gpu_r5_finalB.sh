@@ -1,7 +1,10 @@
 #!/bin/bash
 # Round 5 closing pass B (after pass A's profiles are committed under profiles/r05_pmc/): the bench lines -- the
 # driver's command, the default command, configs 4 and 5, the PPO workload at horizon 16 -> gpurun_out/r5bench/.
+# First the driver shape's PMC passes again with per-launch bytes kept (tools/pmc_summary.py): its refill mean
+# included the second engine's ring-filling launch.
 set -e
+SHAPES=2:fused:20 bash $GRAFT_REPO_ROOT/tools/gpu_r5_profiles.sh
 R=$GRAFT_REPO_ROOT
 cd $R
 O=$R/gpurun_out/r5bench
