@@ -96,6 +96,8 @@ def parse():
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
     ap.add_argument("--eval-episodes", type=int, default=100,
                     help="ppo: deterministic evaluate_policy episodes after the timed iterations (0: none)")
+    ap.add_argument("--host-wait", default="auto", choices=["auto", "spin", "yield"],
+                    help="how the host waits for the GPU (mgx.engine.set_host_wait: hipSetDeviceFlags)")
     ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layouts")
     ap.add_argument("--layout", default=None, choices=["compact", "sb3", "fused"],
                     help="observation storage: compact rows + mgx_gather from one launch per refill epoch "
@@ -580,6 +582,9 @@ def measure_rollout(args, layout, world, rank, dev):
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)                                   # (HIP events are created at their first record:
+    ev1.record(stream)                                   # not inside the region)
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
     for c in range(nchunks):
@@ -824,6 +829,9 @@ def main():
     ndev = torch.cuda.device_count()
     gpu = local % max(ndev, 1)
     backend = os.environ.get("MGX_DIST_BACKEND", "nccl")
+    if args.host_wait != "auto":
+        from mgx.engine import set_host_wait
+        set_host_wait(args.host_wait, gpu)              # before the first GPU work of this process
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if backend == "nccl":

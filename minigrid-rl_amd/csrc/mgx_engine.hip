@@ -540,6 +540,88 @@ __device__ __forceinline__ void render_cols(const uint8_t *grids, int S, int le,
     }
 }
 
+// A whole compact row (byte 0 direction, then the [type 49][colour 49][state 49] frame) of env slot `le`,
+// written as dwords by its 4 threads (round 5; render_cols writes 43 single bytes per thread).  Two passes
+// over the row's own LDS bytes, all four threads of an env being lanes of one wave (LDS operations of a wave
+// complete in order):
+//   1. each thread's columns as render_cols computes them, stored as cell CODES (1 byte per cell) at row
+//      bytes 4 + c, c = vx * 7 + vy;
+//   2. output dword k (row bytes 4k..4k+3) holds four consecutive cells of one plane whose codes are row
+//      bytes 4k - B + 4 .. (B = 1, 50, 99: the plane's first byte), an unaligned window of two code dwords
+//      with a per-plane constant shift (3, 2, 1): thread q's type dwords q + 4j, colour dwords 12 + q + 4j and
+//      state dwords 24 + q + 4j (j < 3; and 36 for q = 0) all take their windows from code dwords q + 4j,
+//      q + 4j + 1, read once.  The three dwords where planes meet (0: direction + types, 12: types + colours,
+//      24: colours + state) are thread 0's.  Decoding is byte-parallel (SWAR) on the window:
+//        t = code & 15; open door (11) -> door (4): t ^ 15 where (t & 0b1011) == 0b1011 (11 is the only such
+//        type present); colour = (code >> 4) & 7; state = 1 + aux (bit 7) where t == 4 -- the one type with
+//        (t & 0b1011) == 0 (no cell code is 0 here: 'unseen' exists only under see_through_walls=False, which
+//        keeps render_cols + apply_vis) -- else 0.
+//   All code reads of the wave are issued before its first output write (they share the row's bytes).
+__device__ __forceinline__ uint32_t swar_type(uint32_t w) {
+    const uint32_t t = w & 0x0F0F0F0Fu, m = ((w & 0x0B0B0B0Bu) + 0x05050505u) & 0x10101010u;
+    return t ^ (m - (m >> 4));                       // 11 -> 11 ^ 15 = 4
+}
+__device__ __forceinline__ uint32_t swar_colour(uint32_t w) { return (w >> 4) & 0x07070707u; }
+__device__ __forceinline__ uint32_t swar_state(uint32_t w) {
+    const uint32_t door = ((((w & 0x0B0B0B0Bu) + 0x0F0F0F0Fu) & 0x10101010u) ^ 0x10101010u) >> 4;   // 0x01 per door byte
+    return door + ((w >> 7) & door);                 // closed 1, locked 2
+}
+template <int EPB = BLOCK_ENVS>
+__device__ __forceinline__ void render_row(const uint8_t *grids, int S, int le, int q, uint32_t rp, uint8_t *row) {
+    const int ax = rp & 0xFF, ay = (rp >> 8) & 0xFF, dir = (rp >> 16) & 3;
+    const uint8_t carry = (uint8_t)(rp >> 24);
+    const int dx = (dir == 0) - (dir == 2), dy = (dir == 1) - (dir == 3);
+    const uint8_t *base = grids + le * 16;
+    uint8_t *cp = row + 4 + 7 * q;                                      // codes of column q (and q + 4)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        if (j == 1 && q == 3) break;
+        const int ox = q + 4 * j - 3;
+        int wx = ax + 6 * dx - __mul24(ox, dy), wy = ay + 6 * dy + __mul24(ox, dx);
+#pragma unroll
+        for (int vy = 0; vy < 7; vy++) {
+            const uint32_t cx = min((uint32_t)wx, (uint32_t)(S - 1)), cy = min((uint32_t)wy, (uint32_t)(S - 1));
+            const int b = (int)__umul24(cy, (uint32_t)S) + (int)cx;
+            uint8_t v = base[b + __mul24(b >> 4, EPB * 16 - 16)];      // cm_off<EPB>(le, b)
+            if (j == 0 && vy == 6 && q == 3) v = carry ? carry : CODE_EMPTY;   // the agent's own cell
+            cp[28 * j + vy] = v;
+            wx -= dx;
+            wy -= dy;
+        }
+    }
+    asm volatile("" ::: "memory");                   // (compiler barriers: the hardware keeps a wave's LDS order)
+    uint32_t *rw = reinterpret_cast<uint32_t *>(row);
+    uint32_t c[8];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        c[2 * j] = rw[q + 4 * j];
+        c[2 * j + 1] = rw[q + 4 * j + 1];
+    }
+    asm volatile("" ::: "memory");
+    uint32_t ty[3], co[3], st[4];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        ty[j] = swar_type(__builtin_amdgcn_alignbyte(c[2 * j + 1], c[2 * j], 3));
+        co[j] = swar_colour(__builtin_amdgcn_alignbyte(c[2 * j + 1], c[2 * j], 2));
+        st[j] = swar_state(__builtin_amdgcn_alignbyte(c[2 * j + 1], c[2 * j], 1));
+    }
+    st[3] = swar_state(__builtin_amdgcn_alignbyte(c[7], c[6], 1));
+    if (q == 0) {
+        // dword 0: direction, types of cells 0-2; 12: types 47, 48 (window of code dwords 12, 13), colours 0, 1;
+        // 24: colours 46-48 (same window, shift 2), state 0
+        ty[0] = (ty[0] & 0xFFFFFF00u) | (uint32_t)dir;
+        co[0] = (co[0] & 0xFFFF0000u) | (swar_type(__builtin_amdgcn_alignbyte(c[7], c[6], 3)) & 0xFFFFu);
+        st[0] = (st[0] & 0xFF000000u) | (swar_colour(__builtin_amdgcn_alignbyte(c[7], c[6], 2)) & 0x00FFFFFFu);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        rw[q + 4 * j] = ty[j];
+        rw[12 + q + 4 * j] = co[j];
+        rw[24 + q + 4 * j] = st[j];
+    }
+    if (q == 0) rw[36] = st[3];
+}
+
 // One env's MiniGridEnv.step + PlaygroundEnv.step (custom_env.py:269-330), as selects: every
 // action's outcome is computed and the taken one kept (a branch per action made a divergent tree of
 // exec-mask updates -- half of the phase's instructions were SALU mask bookkeeping).  The front
@@ -1500,7 +1582,10 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
             if (s_tmask) {
                 // terminal rows (rare, block-uniform): the finished episode's last view, rendered into the
                 // env's frame row from its post-step grid and copied out before the row is reused below
-                if (le < ne && s_term[le]) render_cols<EPB>(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW + 1);
+                if (le < ne && s_term[le]) {
+                    if (VIS) render_cols<EPB>(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW + 1);
+                    else render_row<EPB>(s_grid, S, le, q, s_rpt[le], s_stk + le * FROW);
+                }
                 __syncthreads();
                 if (VIS) {
                     if (tidv < ne && s_term[tidv]) apply_vis(s_stk + tidv * FROW + 1);
@@ -1522,8 +1607,12 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
                 const uint8_t b = s_popb[le];
                 const uint8_t *g = b == 0xFF ? s_grid : s_pg + b * GB;
                 const uint32_t rp = s_rp[le];
-                render_cols<EPB>(g, S, le, q, rp, s_stk + le * FROW + 1);
-                if (q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);
+                if (VIS) {
+                    render_cols<EPB>(g, S, le, q, rp, s_stk + le * FROW + 1);
+                    if (q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);
+                } else {
+                    render_row<EPB>(g, S, le, q, rp, s_stk + le * FROW);
+                }
                 if (b != 0xFF)
                     for (int c = q; c < GSQ; c += 4)
                         *reinterpret_cast<uint4 *>(s_grid + c * (EPB * 16) + le * 16) =

@@ -244,6 +244,28 @@ class MgxEngine:
             pass
 
 
+_HOST_WAIT = {"auto": 0x0, "spin": 0x1, "yield": 0x2}     # hipDeviceSchedule* (hip_runtime_api.h)
+
+
+def set_host_wait(mode, device=None):
+    """How the calling process's host threads wait for `device` (hipSetDeviceFlags): "spin" polls the
+    completion signal (lowest latency from the last kernel's end to `synchronize()` returning, one busy
+    core while waiting), "yield" sleeps on it, "auto" is HIP's default (yield unless there are more HIP
+    contexts than logical CPUs).  A collector that synchronises once per rollout (the reference's
+    `collect_rollouts` reads the rewards back every step) pays the sleeping wait's wake-up on every
+    sync.  Call before the first GPU work on `device`; raises if the runtime refuses the flags."""
+    import os
+    if mode not in _HOST_WAIT:
+        raise ValueError("host wait mode must be one of %s" % sorted(_HOST_WAIT))
+    path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    hip = ctypes.CDLL(path if os.path.exists(path) else "libamdhip64.so")   # the runtime torch loaded
+    dev = device if isinstance(device, int) else (torch.device(device).index or 0) if device is not None else 0
+    for fn, arg in (("hipSetDevice", dev), ("hipSetDeviceFlags", _HOST_WAIT[mode])):
+        rc = getattr(hip, fn)(ctypes.c_int(arg) if fn == "hipSetDevice" else ctypes.c_uint(arg))
+        if rc != 0:
+            raise _lib.MgxError("%s(%d) failed: hipError %d" % (fn, arg, rc))
+
+
 def _check_stats(stats, device=None):
     """The adv-stat triple: f64, >= 3 elements, contiguous, on `device` (the kernel adds to stats[0..2])."""
     if stats is None:
