@@ -1057,7 +1057,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
     if (s_tmask) {
         {
             const int le = tid >> 2, q = tid & 3;
-            if (le < ne && s_term[le]) render_cols(s_grid, S, le, q, s_rp[le], s_stk + le * FSTRIDE + FOFF);
+            if (le < ne && s_term[le]) {
+                if (COMPACT && !p.vis) render_row(s_grid, S, le, q, s_rp[le], s_stk + le * FROW);   // (whole row)
+                else render_cols(s_grid, S, le, q, s_rp[le], s_stk + le * FSTRIDE + FOFF);
+            }
         }
         sync_lds();
         if (p.vis) {
@@ -1093,8 +1096,12 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
         if (le < ne) {
             const bool pop = s_popf[le];
             const uint32_t rp = pop ? (s_phdr[le].x & 0xFFFFFFu) : s_rp[le];   // popped: ax | ay<<8 | dir<<16
-            render_cols(pop ? s_pgrid : s_grid, S, le, q, rp, s_stk + le * FSTRIDE + FOFF);
-            if (COMPACT && q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);   // row byte 0: direction
+            if (COMPACT && !p.vis) {                  // the whole row as dwords, direction included (render_row)
+                render_row(pop ? s_pgrid : s_grid, S, le, q, rp, s_stk + le * FROW);
+            } else {
+                render_cols(pop ? s_pgrid : s_grid, S, le, q, rp, s_stk + le * FSTRIDE + FOFF);
+                if (COMPACT && q == 0) s_stk[le * FROW] = (uint8_t)((rp >> 16) & 3);   // row byte 0: direction
+            }
         }
     }
     // COMPACT without process_vis: each wave copies out the 16 rows it rendered itself (below),
