@@ -76,11 +76,11 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="replay the timed steps from a hipGraph")
     ap.add_argument("--probe", type=int, default=256, help="eager steps timed per launch for the roofline")
     ap.add_argument("--workload", default="rollout", choices=["rollout", "ppo"])
-    ap.add_argument("--gae-fused", type=int, default=0,
+    ap.add_argument("--gae-fused", type=int, default=1,
                     help="fused layout with one launch per horizon (E = H): 1 = GAE in the rollout launch "
-                         "(mgx_rollout_compact_gae); 0 = a separate mgx_gae_dones launch (default: the same "
-                         "speed on the driver's line in round 4's A/B, and the separate kernel is the one the "
-                         "per-step layouts use)")
+                         "(mgx_rollout_compact_gae; round 5: +2 %% on the driver's line over the separate kernels, "
+                         "which cost two more launches on the rollout's branch of the graph); 0 = a separate "
+                         "mgx_gae_dones launch + its fold")
     ap.add_argument("--refill-every", type=int, default=0, help="steps per refill epoch (0 = engine default, D/4)")
     ap.add_argument("--min-warmup", type=int, default=256,
                     help="rollout: the warm-up is at least this many steps (whole refill epochs)")
@@ -96,8 +96,10 @@ def parse():
     ap.add_argument("--epochs", type=int, default=4, help="ppo: n_epochs")
     ap.add_argument("--eval-episodes", type=int, default=100,
                     help="ppo: deterministic evaluate_policy episodes after the timed iterations (0: none)")
-    ap.add_argument("--host-wait", default="auto", choices=["auto", "spin", "yield"],
-                    help="how the host waits for the GPU (mgx.engine.set_host_wait: hipSetDeviceFlags)")
+    ap.add_argument("--host-wait", default="spin", choices=["auto", "spin", "yield"],
+                    help="how the host waits for the GPU (mgx.engine.set_host_wait: hipSetDeviceFlags); spin: "
+                         "the synchronize() that closes the region returns ~10-20 us sooner after the last kernel "
+                         "(round 5: +3 %% on the driver's 20-step line), one busy host core per rank")
     ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layouts")
     ap.add_argument("--layout", default=None, choices=["compact", "sb3", "fused"],
                     help="observation storage: compact rows + mgx_gather from one launch per refill epoch "
@@ -316,7 +318,7 @@ def main_ppo(args, world, rank, local, dev, ranks_seen=1):
                        "horizon": cfg.horizon, "batch_size": cfg.batch_size, "n_epochs": cfg.n_epochs,
                        "minibatches_per_epoch": n * world * cfg.horizon // cfg.batch_size // world,
                        "mission_cache": cfg.mission_cache, "layout": cfg.layout,
-                       "parallelism": "env-sharded dp%d" % world},
+                       "parallelism": "env-sharded dp%d" % world, "host_wait": getattr(args, "host_wait_applied", "auto")},
             "phases_s_per_iter": {"collect": tc / K, "train": tt / K},
             "eval": ev,
             "roofline": None,
@@ -682,6 +684,9 @@ def measure_rollout(args, layout, world, rank, dev):
         probe_s = (sum(probe_us) / len(probe_us)) * 1e-6 if probe_us else None
         resets_per_launch = (st1["resets"] - st0["resets"]) / K
         b_alg = B_STEP * n + (3 * args.size ** 2 + 208) * resets_per_launch
+        gae_in = fused and E == H and args.gae_fused
+        if gae_in:                                       # the launch also runs GAE over its steps: SURVEY 8(d)'s
+            b_alg += 17 * n                              # 17 B per element (r, v, done, adv, ret), per step
         # THE roofline duration: the kernel's own launches inside the timed region, per step, from the device
         # clock (first workgroup start -> last workgroup end of each launch; the max over ranks)
         per_launch_s = step_us_max * 1e-6
@@ -760,6 +765,7 @@ def measure_rollout(args, layout, world, rank, dev):
                        "problem": args.problem, "mission": mission, "size": args.size, "num_objects": 4,
                        "envs_per_gpu": n, "n_stack": args.n_stack, "parallelism": "env-sharded dp%d" % world,
                        "hipgraph": bool(graphs), "refill_every": E, "horizon": H, "layout": layout,
+                       "host_wait": getattr(args, "host_wait_applied", "auto"),
                        "timed": "%d steps = %d whole refill epochs%s; GAE + adv-stat %s every %d steps%s" % (
                            K, K // E, "" if aligned else " + a joined partial one",
                            "all-reduce (%s)" % dist.get_backend() if world > 1 else "accumulation", H,
@@ -775,8 +781,9 @@ def measure_rollout(args, layout, world, rank, dev):
                        "carry_over": "ring rows (no copy)" if compact else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": ("mgx_rollout_kernel<false> (fused: %d steps per launch; per-step figures = "
-                                    "launch / %d)" % (E, E) if fused else
+                         "kernel": ("mgx_rollout_kernel<false> (fused: %d steps per launch%s; per-step figures = "
+                                    "launch / %d)" % (E, ", GAE epilogue: B_alg + 17 B per env-step" if gae_in else "",
+                                                      E) if fused else
                                     "mgx_step_kernel<int, true[, 8]> (compact)" if compact else
                                     "mgx_step_kernel<int, false[, 8]> (SB3 stacks)"),
                          "avg_launch_us": per_launch_s * 1e6,
@@ -829,9 +836,15 @@ def main():
     ndev = torch.cuda.device_count()
     gpu = local % max(ndev, 1)
     backend = os.environ.get("MGX_DIST_BACKEND", "nccl")
+    args.host_wait_applied = "auto"
     if args.host_wait != "auto":
+        from mgx import MgxError
         from mgx.engine import set_host_wait
-        set_host_wait(args.host_wait, gpu)              # before the first GPU work of this process
+        try:
+            set_host_wait(args.host_wait, gpu)          # before the first GPU work of this process
+            args.host_wait_applied = args.host_wait
+        except MgxError as ex:                          # (the line is still printed; it says which wait it ran)
+            print("bench: host wait %s refused (%s); HIP's default" % (args.host_wait, ex), file=sys.stderr)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if backend == "nccl":

@@ -49,3 +49,16 @@ def test_committed_profiles_reproduce_the_driver_line_roofline():
     # a window of launches outside the trace is refused, not averaged
     assert bench._rocprof_trace_timed_avg(os.path.join(d, "kernel_trace_2_fused_e20.csv.gz"),
                                           "mgx_rollout_kernel", 10 ** 6, 1) is None
+
+
+def test_host_wait_modes_and_defaults():
+    """bench.py's defaults (round 5): spin-waiting host, GAE fused into the rollout launch; an unknown wait mode
+    is refused before anything touches the HIP runtime."""
+    import pytest
+    sys.argv = ["bench.py"]
+    a = bench.parse()
+    assert a.host_wait == "spin" and a.gae_fused == 1
+    sys.path.insert(0, os.path.join(bench.ROOT, "minigrid-rl_amd"))
+    from mgx.engine import set_host_wait
+    with pytest.raises(ValueError):
+        set_host_wait("busy")
