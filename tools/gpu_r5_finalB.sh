@@ -1,10 +1,8 @@
 #!/bin/bash
 # Round 5 closing pass B (after pass A's profiles are committed under profiles/r05_pmc/): the bench lines -- the
 # driver's command, the default command, configs 4 and 5, the PPO workload at horizon 16 -> gpurun_out/r5bench/.
-# First the driver shape's PMC passes again with per-launch bytes kept (tools/pmc_summary.py): its refill mean
-# included the second engine's ring-filling launch.
+# Then the N > 1 rehearsal (tools/gpu_dp_rehearsal.sh: gloo ranks on the one GPU).
 set -e
-SHAPES=2:fused:20 bash $GRAFT_REPO_ROOT/tools/gpu_r5_profiles.sh
 R=$GRAFT_REPO_ROOT
 cd $R
 O=$R/gpurun_out/r5bench
@@ -17,3 +15,4 @@ timeout -k 10 500 python bench.py --workload ppo --steps 2 --warmup 1 --horizon 
 for f in $O/bench*.json; do python3 -c "
 import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{\"metric')][0]); r=d.get('roofline') or {}
 print('$f'.split('/')[-1], '%.3e' % d['value'], d['ms_per_step'], 'frac', r.get('frac'), 'traffic', r.get('traffic'), 'rocprof', (r.get('rocprof') or {}).get('timed_frac'))"; done
+bash $R/tools/gpu_dp_rehearsal.sh
