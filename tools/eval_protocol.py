@@ -23,6 +23,19 @@ import torch  # noqa: E402
 COLUMNS = (("GTG", 5), ("GTO", 0), ("PKP", 2), ("TGL", 1), ("ALL", None))
 
 
+def protocol_column(model, mission, episodes=1000, size=8, seed=42, dev=None):
+    """One README.md:54-65 column under test(): a 1-env engine seeded `seed`, `episodes` sequential deterministic
+    episodes (mgx.evaluate_test_protocol), summarised per task and per (task, room count) cell."""
+    from mgx import MgxEngine, evaluate_test_protocol
+    from mgx.evaluation import summarize_episodes
+    eng = MgxEngine(problem="multi", mission=mission, size=size, num_objects=4, n_envs=1, seed=seed, n_stack=4,
+                    terminal_mode="none", reward64=True, mission_dtype=torch.uint8, device=dev or "cuda")
+    try:
+        return summarize_episodes(evaluate_test_protocol(model, eng, episodes, deterministic=True))
+    finally:
+        eng.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ckpt", default=None)
@@ -34,8 +47,7 @@ def main():
     ap.add_argument("--fresh", type=int, default=1, help="also round 4's fresh-engine method, for comparison")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
-    from mgx import MgxEngine, evaluate_policy, evaluate_test_protocol
-    from mgx.evaluation import summarize_episodes
+    from mgx import MgxEngine, evaluate_policy
     from mgx.policy import ActorCriticPolicy
     dev = torch.device("cuda:0")
     ck = None
@@ -60,11 +72,7 @@ def main():
         if name not in want:
             continue
         t0 = time.perf_counter()
-        eng = MgxEngine(problem="multi", mission=mission, size=args.size, num_objects=4, n_envs=1, seed=args.seed,
-                        n_stack=4, terminal_mode="none", reward64=True, mission_dtype=torch.uint8, device=dev)
-        eps = evaluate_test_protocol(model, eng, args.episodes, deterministic=True)
-        eng.close()
-        col = summarize_episodes(eps)
+        col = protocol_column(model, mission, args.episodes, args.size, args.seed, dev)
         col["seconds"] = round(time.perf_counter() - t0, 1)
         if args.fresh:
             # round 4's method: n_envs = episodes fresh envs, one episode each (one (mission, rooms) cell)

@@ -1,7 +1,8 @@
 """BASELINE config 3 learning evidence: PPO (mgx.ppo.learn: the reference's PPO(CustomPPOPolicy,
-vec_env).learn restated over the engine) on PKP 8x8, then the success rate over 1,000 deterministic
-evaluation episodes on a fresh engine (README.md:54-65 "Benchmark (1k ep)": success = the episode
-paid a reward, i.e. the mission was completed; the reference reports PKP 57%).
+vec_env).learn restated over the engine) on PKP 8x8 (or --mission), then the success rate over 1,000
+deterministic episodes under the reference's test() protocol (README.md:54-65 "Benchmark (1k ep)": one env
+seeded 42, sequential episodes; success = the episode paid a reward, i.e. the mission was completed; the
+reference reports PKP 57%).
 
 The reference trains 16 envs x horizon 1024 with minibatch 256 (algorithm/ppo.yaml); at 65,536 envs
 the same update count per sample would take 16,384 optimiser steps per 16-step rollout, so this run
@@ -23,22 +24,22 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
-def success_rate(policy, env_kw, n_episodes, seed, deterministic=True):
-    from mgx import MgxEngine, evaluate_policy
-    eng = MgxEngine(n_envs=n_episodes, seed=seed, n_stack=4, terminal_mode="none", reward64=True,
-                    mission_dtype=torch.uint8, **env_kw)
-    if policy is None:                                  # uniform random actions (reference point)
-        g = torch.Generator(device=eng.device)
+def success_rate(policy, env_kw, n_episodes, seed=42):
+    """README.md:54-65's success rate under the reference's own test() protocol (src/ppo.py:185-230; round 5,
+    ADVICE r4): ONE env seeded `seed`, `n_episodes` sequential deterministic episodes, the MT19937 stream advancing
+    -- tools/eval_protocol.py's column.  (Round 4 ran one episode on each of N fresh envs: every env's first episode
+    draws the same mission and room count, one (task, rooms) cell.)  policy None: uniform random actions."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from eval_protocol import protocol_column
+    if policy is None:
+        g = torch.Generator(device="cuda")
         g.manual_seed(seed)
-        act = lambda obs: torch.randint(0, 7, (eng.n,), device=eng.device, generator=g)   # noqa: E731
-        rews, lens = evaluate_policy(act, eng, n_episodes, return_episode_rewards=True)
+        model = lambda obs: torch.randint(0, 7, (obs["image"].shape[0],), device="cuda", generator=g)   # noqa: E731
     else:
         policy.train(False)
-        rews, lens = evaluate_policy(policy, eng, n_episodes, deterministic=deterministic, return_episode_rewards=True)
-    eng.close()
-    r = np.asarray(rews)
-    return dict(episodes=int(r.size), success_rate=float((r > 0).mean()), mean_reward=float(r.mean()),
-                mean_length=float(np.mean(lens)))
+        model = policy
+    col = protocol_column(model, env_kw.get("mission"), n_episodes, env_kw.get("size", 8), seed)
+    return dict(col["overall"], per_task=col["per_task"], per_cell=col["per_cell"])
 
 
 def main():
@@ -88,7 +89,7 @@ def main():
                     f.write(json.dumps(curve[-1]) + "\n")
             if len(curve) % 10 == 1:
                 print("t=%.0fs %s" % (time.perf_counter() - t0, json.dumps(curve[-1])), file=sys.stderr, flush=True)
-    random_eval = None if args.no_eval else success_rate(None, env_kw, args.eval_episodes, seed=4242)
+    random_eval = None if args.no_eval else success_rate(None, env_kw, args.eval_episodes)
     t_start = time.perf_counter()
     pol, hist, eng = learn(cfg, int(args.timesteps), log=log, callback=Stop(), init=init)
     train_s = prior_s + time.perf_counter() - t_start
@@ -101,13 +102,14 @@ def main():
         print(json.dumps({"segment": segment, "timesteps": steps_done, "train_seconds": train_s,
                           "last": curve[-1] if curve else None}))
         return
-    ev = success_rate(pol, env_kw, args.eval_episodes, seed=4242)
+    ev = success_rate(pol, env_kw, args.eval_episodes)
     names = {2: "PKP", 5: "GTG", 0: "GTO", 1: "TGL", None: "ALL"}
     # README.md:54-65's table: the model evaluated on every task (columns GTG GTO PKP TGL ALL)
-    per_task = {names[m]: success_rate(pol, dict(env_kw, mission=m), args.eval_episodes, seed=4242)
-                for m in (5, 0, 2, 1, None)} if mission is None else None
-    out = {"what": "PPO (mgx.ppo.learn) on %s, then evaluate_policy over %d deterministic episodes on a fresh "
-                   "engine (seed 4242)" % (names.get(mission, "mission %s" % mission), args.eval_episodes),
+    per_task = {names[m]: success_rate(pol, dict(env_kw, mission=m), args.eval_episodes)
+                for m in (5, 0, 2, 1)} if mission is None else None
+    out = {"what": "PPO (mgx.ppo.learn) on %s, then the reference's test() protocol: one env seeded 42, %d "
+                   "sequential deterministic episodes (tools/eval_protocol.py)" % (names.get(mission, "mission %s" % mission),
+                                                                                   args.eval_episodes),
            "eval_per_task": per_task,
            "config": {"env": env_kw, "n_envs": cfg.n_envs, "horizon": cfg.horizon, "batch_size": cfg.batch_size,
                       "n_epochs": cfg.n_epochs, "optimizer_steps_per_rollout": cfg.n_epochs * cfg.n_envs *
@@ -120,7 +122,9 @@ def main():
            "reference": ("README.md:65 PPO ALL model: GTG 75%, GTO 65%, PKP 59%, TGL 58%, ALL 65% (1k episodes; trained "
                          "through the all0..all6 curriculum, README.md:40-46; size and training steps unstated)"
                          if mission is None else
-                         "README.md:61 PPO PKP model on PKP: 57% (1k episodes; size and training steps unstated)"),
+                         {5: "README.md:59 PPO GTG model: GTG 86%, ALL 19%", 0: "README.md:60 PPO GTO model: GTO 72%, ALL 17%",
+                          2: "README.md:61 PPO PKP model: PKP 57%, ALL 26%", 1: "README.md:63 PPO TGL model: TGL 47%, ALL 27%"
+                          }.get(mission, "") + " (1k episodes; size and training steps unstated)"),
            "curve": curve[::max(1, len(curve) // 40)]}
     print(json.dumps(out))
     if args.out:
