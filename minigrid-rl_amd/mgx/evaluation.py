@@ -94,7 +94,7 @@ def task_of(mission_text):
 
 
 @torch.no_grad()
-def evaluate_test_protocol(model, engine, n_episodes=1000, deterministic=True):
+def evaluate_test_protocol(model, engine, n_episodes=1000, deterministic=True, progress=None):
     """The reference's benchmark protocol, `test()` (src/ppo.py:185-230; README.md:54-65 "Benchmark (1k ep)"):
     ONE env, make_vec_env(make_env, n_envs=1, seed=cfg.seed, vec_env_cls=DummyVecEnv) + VecTransposeImage +
     VecFrameStack, and per episode
@@ -108,7 +108,8 @@ def evaluate_test_protocol(model, engine, n_episodes=1000, deterministic=True):
     it is done (one episode generated), and test()'s next vec_env.reset() -- unseeded, both streams continuing --
     generates another (MgxEngine.reset after the first is that unseeded reset).
     Returns one dict per episode: reward (f64 sum), length, success (reward > 0: the mission was completed),
-    mission_id, mission text, task (README's column), rooms (multi: 2 / 3 / 4 from the door count; else 0)."""
+    mission_id, mission text, task (README's column), rooms (multi: 2 / 3 / 4 from the door count; else 0).
+    `progress(k)`, if given, is called after every episode (k episodes done)."""
     from ._lib import mission_text
     if engine.n != 1:
         raise ValueError("the test() protocol steps ONE env (src/ppo.py:201-206: n_envs=1)")
@@ -131,6 +132,8 @@ def evaluate_test_protocol(model, engine, n_episodes=1000, deterministic=True):
                 break
         out.append(dict(reward=total, length=length, success=total > 0, mission_id=mid, mission=texts[mid],
                         task=task_of(texts[mid]), rooms=_ROOMS_BY_DOORS.get(doors, 0)))
+        if progress is not None:
+            progress(len(out))
     return out
 
 

@@ -31,7 +31,10 @@ def protocol_column(model, mission, episodes=1000, size=8, seed=42, dev=None):
     eng = MgxEngine(problem="multi", mission=mission, size=size, num_objects=4, n_envs=1, seed=seed, n_stack=4,
                     terminal_mode="none", reward64=True, mission_dtype=torch.uint8, device=dev or "cuda")
     try:
-        return summarize_episodes(evaluate_test_protocol(model, eng, episodes, deterministic=True))
+        def progress(k):                                  # (a line a minute or so: a silent GPU run looks hung)
+            if k % 100 == 0:
+                print("  %d / %d episodes" % (k, episodes), file=sys.stderr, flush=True)
+        return summarize_episodes(evaluate_test_protocol(model, eng, episodes, deterministic=True, progress=progress))
     finally:
         eng.close()
 
