@@ -82,6 +82,12 @@ def parse():
                          "which cost two more launches on the rollout's branch of the graph); 0 = a separate "
                          "mgx_gae_dones launch + its fold")
     ap.add_argument("--refill-every", type=int, default=0, help="steps per refill epoch (0 = engine default, D/4)")
+    ap.add_argument("--warmup-ms", type=float, default=0.0,
+                    help="rollout: untimed graph replays continue until the warm-up has run this long (0: one "
+                         "replay of each graph, the rings still nearly full: see --steady-ms)")
+    ap.add_argument("--steady-ms", type=float, default=400.0,
+                    help="rollout, N=1: after everything else, this much more of untimed replays, then the same "
+                         "steps timed again -> `steady_state` beside the headline (0: skip)")
     ap.add_argument("--min-warmup", type=int, default=256,
                     help="rollout: the warm-up is at least this many steps (whole refill epochs)")
     ap.add_argument("--refill-cap", type=int, default=0, help="extra episodes per env per epoch (0 = engine default)")
@@ -100,6 +106,10 @@ def parse():
                     help="how the host waits for the GPU (mgx.engine.set_host_wait: hipSetDeviceFlags); spin: "
                          "the synchronize() that closes the region returns ~10-20 us sooner after the last kernel "
                          "(round 5: +3 %% on the driver's 20-step line), one busy host core per rank")
+    ap.add_argument("--graph-launch", default="torch", choices=["raw", "torch"],
+                    help="timed graph replays: torch's CUDAGraph.replay(), or hipGraphLaunch on the graph exec "
+                         "(mgx.engine.graph_launch: without replay()'s ~9 us of host bookkeeping; round 5 A/B: "
+                         "no difference on the driver's line, 6.04-6.18 vs 5.95-6.23 x 10^9)")
     ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layouts")
     ap.add_argument("--layout", default=None, choices=["compact", "sb3", "fused"],
                     help="observation storage: compact rows + mgx_gather from one launch per refill epoch "
@@ -508,6 +518,7 @@ def measure_rollout(args, layout, world, rank, dev):
     gamma, lam = 0.8108071290665859, 0.9452281119742252
     eng.reset()
     stream = torch.cuda.current_stream(dev)
+    t_warm0 = time.perf_counter()
     if compact:
         cbuf.observe(0)
         for t in range(0, W, E if fused else 1):
@@ -549,6 +560,7 @@ def measure_rollout(args, layout, world, rank, dev):
                                                          # pays for every refill it forked
 
     graphs = []
+    replay_cycles = 1                                    # untimed replays of the graph set (warm-up)
     forks0 = eng.stats()["refill_launches"]
     # ring buffer: graph c writes block (c0 + c + 1) % m; replayed in cyclic order, the graphs continue the
     # block sequence only if there is a multiple of m of them (one 20-step chunk -> two graphs, alternating)
@@ -573,6 +585,15 @@ def measure_rollout(args, layout, world, rank, dev):
         for gr in graphs:
             gr.replay()
         torch.cuda.synchronize(dev)
+        # then whole cycles of untimed replays until the warm-up has kept the GPU busy for --warmup-ms: a few ms of
+        # warm-up left the first bench of a fresh process (kernel 8.9 vs 7.6 us per step) on a box whose
+        # clocks had not settled
+        while (time.perf_counter() - t_warm0) * 1e3 < args.warmup_ms:
+            for gr in graphs:
+                gr.replay()
+            torch.cuda.synchronize(dev)
+            replay_cycles += 1
+    eng.clock_rewind()                                   # (the slots then hold the region's and the probe's launches)
     st0 = eng.stats()
     # refill launches inside the timed region: the forks the steps enqueued (captured once in the
     # graphs, replayed once each; eagerly, counted as they run)
@@ -587,11 +608,16 @@ def measure_rollout(args, layout, world, rank, dev):
     ev0.record(stream)                                   # (HIP events are created at their first record:
     ev1.record(stream)                                   # not inside the region)
     torch.cuda.synchronize(dev)
+    from mgx.engine import graph_launch
+    raw = args.graph_launch == "raw"
     t0 = time.perf_counter()
     ev0.record(stream)
     for c in range(nchunks):
         if graphs:
-            graphs[c].replay()
+            if raw:
+                graph_launch(graphs[c], stream)
+            else:
+                graphs[c].replay()
         else:
             chunk(c)
         if world > 1:                                    # the one exchange per rollout
@@ -680,6 +706,38 @@ def measure_rollout(args, layout, world, rank, dev):
     assert abs(hs[:, 2].sum() - float(H) * n * world * nchunks) < 0.5, hs    # every chunk's GAE ran
     gae_h = gae_probe(dev, n, H)
     gae_1k = gae_probe(dev, n, 1024) if H != 1024 else gae_h
+    # Steady state (round 5, reported beside the headline, N = 1): the same graphs after --steady-ms more of
+    # untimed replays, then several timed replays.  The region above follows mgx_reset by a few hundred steps, when
+    # every ring is still nearly full; over thousands of steps an env in a long live-lock streak (reset_env's
+    # retries, each an abandoned attempt) drains its ring to the 2K floor, and from then on its wave runs
+    # need-driven retry rounds every epoch -- the slowest wave sets the refill launch.
+    steady = None
+    if graphs and world == 1 and args.steady_ms > 0 and layout == args.layout:
+        t_s = time.perf_counter()
+        cyc = 0
+        while (time.perf_counter() - t_s) * 1e3 < args.steady_ms:
+            for gr in graphs:
+                gr.replay()
+            torch.cuda.synchronize(dev)
+            cyc += 1
+        reps = max(1, 200 // K)
+        sa = eng.stats()
+        torch.cuda.synchronize(dev)
+        t0s = time.perf_counter()
+        for _ in range(reps):
+            for c in range(nchunks):
+                graphs[c].replay()
+        torch.cuda.synchronize(dev)
+        wall_s = time.perf_counter() - t0s
+        sb = eng.stats()
+        prod_s = (sb["resets"] - sa["resets"]) + (sb["queued"] - sa["queued"])
+        cons_s = sb["resets"] - sa["resets"]
+        steady = {"value": n * K * reps / wall_s, "ms_per_step": wall_s * 1e3 / (K * reps),
+                  "timed_steps": K * reps, "after_steps": W + (replay_cycles + cyc) * len(graphs) * H + K,
+                  "produced_over_consumed": prod_s / max(cons_s, 1),
+                  "note": "the region's graphs replayed %d more cycles (%.0f ms) untimed, then %d times timed: the "
+                          "rings' steady state (a few hundred steps after mgx_reset they are still nearly full)"
+                          % (cyc, args.steady_ms, reps)}
     if rank == 0:
         probe_s = (sum(probe_us) / len(probe_us)) * 1e-6 if probe_us else None
         resets_per_launch = (st1["resets"] - st0["resets"]) / K
@@ -745,12 +803,13 @@ def measure_rollout(args, layout, world, rank, dev):
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
-            "warmup": W + (K if graphs else 0),          # + one untimed replay of the graphs
+            "warmup": W + (replay_cycles * len(graphs) * H if graphs else 0),   # + the graphs' untimed replays
             "warmup_requested": args.warmup,
-            "warmup_note": "warm-up raised to >= %d steps in whole refill epochs (+ one untimed replay of "
-                           "each graph): every env starts its first episode at the reset, and the reset rate "
-                           "the timed window pays for (`window`) settles only after a few max_steps; a window "
-                           "right after the reset would see fewer resets than steady state" % args.min_warmup,
+            "warmup_note": "warm-up raised to >= %d steps in whole refill epochs, then untimed replays of the "
+                           "graphs (%d cycles; --warmup-ms %.0f): every env starts its first episode at the "
+                           "reset, and the reset rate the timed window pays for (`window`) settles only after a few "
+                           "max_steps; the rings are still nearly full then (`steady_state`: thousands of steps "
+                           "later)" % (args.min_warmup, replay_cycles, args.warmup_ms),
             "ms_per_step": wall_max * 1e3 / K,
             "higher_is_better": True,
             "scaling": "weak",
@@ -766,6 +825,8 @@ def measure_rollout(args, layout, world, rank, dev):
                        "envs_per_gpu": n, "n_stack": args.n_stack, "parallelism": "env-sharded dp%d" % world,
                        "hipgraph": bool(graphs), "refill_every": E, "horizon": H, "layout": layout,
                        "host_wait": getattr(args, "host_wait_applied", "auto"),
+                       "graph_launch": ("hipGraphLaunch" if args.graph_launch == "raw" else "CUDAGraph.replay")
+                       if graphs else None,
                        "timed": "%d steps = %d whole refill epochs%s; GAE + adv-stat %s every %d steps%s" % (
                            K, K // E, "" if aligned else " + a joined partial one",
                            "all-reduce (%s)" % dist.get_backend() if world > 1 else "accumulation", H,
@@ -817,6 +878,7 @@ def measure_rollout(args, layout, world, rank, dev):
                          "stack_bytes_per_launch": stack_bytes,
                          "achieved_incl_stack": (b_alg + stack_bytes) / per_launch_s / 1e9},
             "gae": {"horizon": gae_h, "T1024": gae_1k},
+            "steady_state": steady,
             "gpu_time_ms": gpu_max * 1e3,
         }
         return out

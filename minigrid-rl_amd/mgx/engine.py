@@ -176,6 +176,13 @@ class MgxEngine:
             off += g * (1 + 2 * self.clock_slots)
         return self.clock
 
+    def clock_rewind(self):
+        """Forget every recorded launch (counters and records to zero), e.g. after a warm-up, so that the slots
+        hold the launches that follow.  Call with no kernel of this engine in flight (synchronises first)."""
+        torch.cuda.synchronize(self.device)
+        self.clock.zero_()
+        torch.cuda.synchronize(self.device)
+
     def clock_launches(self, cls=0):
         """Launches of kernel class `cls` so far (synchronises)."""
         torch.cuda.synchronize(self.device)
@@ -245,6 +252,29 @@ class MgxEngine:
 
 
 _HOST_WAIT = {"auto": 0x0, "spin": 0x1, "yield": 0x2}     # hipDeviceSchedule* (hip_runtime_api.h)
+_HIP = None
+
+
+def _hip():
+    """The HIP runtime torch loaded (libamdhip64 of torch/lib, else the system one)."""
+    global _HIP
+    if _HIP is None:
+        import os
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        _HIP = ctypes.CDLL(path if os.path.exists(path) else "libamdhip64.so")
+        _HIP.hipGraphLaunch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        _HIP.hipGraphLaunch.restype = ctypes.c_int
+    return _HIP
+
+
+def graph_launch(graph, stream):
+    """Launch an instantiated torch.cuda.CUDAGraph on `stream` with hipGraphLaunch directly: the same work as
+    graph.replay() without its per-call bookkeeping (device guards, capture checks, RNG-offset updates --
+    ~9 us of host time before the launch, HIP API trace of bench.py).  Only for graphs that captured no torch
+    random-number op (whose Philox offsets replay() advances): the engine's rollouts, GAE and gathers qualify."""
+    rc = _hip().hipGraphLaunch(ctypes.c_void_p(graph.raw_cuda_graph_exec()), ctypes.c_void_p(stream.cuda_stream))
+    if rc != 0:
+        raise _lib.MgxError("hipGraphLaunch failed: hipError %d" % rc)
 
 
 def set_host_wait(mode, device=None):
@@ -254,11 +284,9 @@ def set_host_wait(mode, device=None):
     contexts than logical CPUs).  A collector that synchronises once per rollout (the reference's
     `collect_rollouts` reads the rewards back every step) pays the sleeping wait's wake-up on every
     sync.  Call before the first GPU work on `device`; raises if the runtime refuses the flags."""
-    import os
     if mode not in _HOST_WAIT:
         raise ValueError("host wait mode must be one of %s" % sorted(_HOST_WAIT))
-    path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
-    hip = ctypes.CDLL(path if os.path.exists(path) else "libamdhip64.so")   # the runtime torch loaded
+    hip = _hip()                                     # the runtime torch loaded
     dev = device if isinstance(device, int) else (torch.device(device).index or 0) if device is not None else 0
     for fn, arg in (("hipSetDevice", dev), ("hipSetDeviceFlags", _HOST_WAIT[mode])):
         rc = getattr(hip, fn)(ctypes.c_int(arg) if fn == "hipSetDevice" else ctypes.c_uint(arg))

@@ -36,6 +36,7 @@ declare -A V=(
   [slprio3]="-DMGX_STEP_LOGIC_PRIO=3"
   [lp3sf]="-DMGX_ROLL_LOGIC_PRIO=3 -DMGX_SLIDE_FENCE=1"
   [lp3sfrx]="-DMGX_ROLL_LOGIC_PRIO=3 -DMGX_SLIDE_FENCE=1 -DMGX_PUBN_ACQUIRE=0"
+  [rclock_np]="-DMGX_REFILL_CLOCK=1"
   [gskip1]="-DMGX_GEN_SKIP=1"
   [gskip2]="-DMGX_GEN_SKIP=2"
   [gskip4]="-DMGX_GEN_SKIP=4"
