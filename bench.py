@@ -708,9 +708,8 @@ def measure_rollout(args, layout, world, rank, dev):
     gae_1k = gae_probe(dev, n, 1024) if H != 1024 else gae_h
     # Steady state (round 5, reported beside the headline, N = 1): the same graphs after --steady-ms more of
     # untimed replays, then several timed replays.  The region above follows mgx_reset by a few hundred steps, when
-    # every ring is still nearly full; over thousands of steps an env in a long live-lock streak (reset_env's
-    # retries, each an abandoned attempt) drains its ring to the 2K floor, and from then on its wave runs
-    # need-driven retry rounds every epoch -- the slowest wave sets the refill launch.
+    # every ring is still nearly full; over thousands of steps a few rings drain to the 2K floor and their waves
+    # run need-driven rounds every epoch -- the slowest wave sets the refill launch.
     steady = None
     if graphs and world == 1 and args.steady_ms > 0 and layout == args.layout:
         t_s = time.perf_counter()
