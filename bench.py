@@ -86,8 +86,11 @@ def parse():
                     help="rollout: untimed graph replays continue until the warm-up has run this long (0: one "
                          "replay of each graph, the rings still nearly full: see --steady-ms)")
     ap.add_argument("--steady-ms", type=float, default=400.0,
-                    help="rollout, N=1: after everything else, this much more of untimed replays, then the same "
+                    help="rollout: after everything else, this much more of untimed replays, then the same "
                          "steps timed again -> `steady_state` beside the headline (0: skip)")
+    ap.add_argument("--steady-steps", type=int, default=20480,
+                    help="rollout: untimed graph replays continue until this many steps after mgx_reset, so that the "
+                         "timed region sits in the rings' steady state (round 6; 0: one replay of each graph)")
     ap.add_argument("--min-warmup", type=int, default=256,
                     help="rollout: the warm-up is at least this many steps (whole refill epochs)")
     ap.add_argument("--refill-cap", type=int, default=0, help="extra episodes per env per epoch (0 = engine default)")
@@ -110,6 +113,9 @@ def parse():
                     help="timed graph replays: torch's CUDAGraph.replay(), or hipGraphLaunch on the graph exec "
                          "(mgx.engine.graph_launch: without replay()'s ~9 us of host bookkeeping; round 5 A/B: "
                          "no difference on the driver's line, 6.04-6.18 vs 5.95-6.23 x 10^9)")
+    ap.add_argument("--mark-region", type=int, default=0,
+                    help="a torch.cuda._sleep kernel right before and after the timed region (kernel-trace marker for "
+                         "tools/trace_window.py; outside the region)")
     ap.add_argument("--both-layouts", type=int, default=1, help="rollout, N=1: also time the other layouts")
     ap.add_argument("--layout", default=None, choices=["compact", "sb3", "fused"],
                     help="observation storage: compact rows + mgx_gather from one launch per refill epoch "
@@ -133,7 +139,7 @@ def parse():
     if args.layout is None:
         # rollout: the fused launch per refill epoch (the actions of a random-action rollout are known
         # up front); it needs the timed steps to be whole epochs (pick_epoch), else one launch per step
-        args.layout = "compact" if ppo or pick_epoch(args.steps, args.ring_depth or 256) is None else "fused"
+        args.layout = "compact" if ppo or pick_epoch(args.steps, args.ring_depth or 512) is None else "fused"
     return args
 
 
@@ -407,7 +413,7 @@ def _profile_dir():
     return None, sha
 
 
-def pick_epoch(K, D=256):
+def pick_epoch(K, D=512):
     """Refill epoch E (mgx refill_every) so that the K timed steps are whole epochs: the largest
     divisor of K in [8, min(64, D/4)] (at D/2 the ring invariant 2E <= D makes every epoch refill the
     rings to full, so each wave runs as many rounds as its busiest lane consumed; at <= D/4 the
@@ -465,7 +471,7 @@ def measure_rollout(args, layout, world, rank, dev):
     n = args.n_envs
     mission = None if args.mission == "None" else int(args.mission)
     K = args.steps
-    D = args.ring_depth or 256
+    D = args.ring_depth or 512
     E = args.refill_every or pick_epoch(K, D)
     aligned = E is not None and K % E == 0
     eng = MgxEngine(problem=args.problem, mission=mission, size=args.size, n_envs=n, seed=42,
@@ -536,22 +542,26 @@ def measure_rollout(args, layout, world, rank, dev):
     torch.cuda.synchronize(dev)                          # captures (no cross-capture dependency)
     assert eng.calls % E == 0                            # the timed region starts on an epoch boundary
 
-    def chunk(c):
+    def chunk(c, acts=None, device_policy=False):
+        # acts: the chunk's [H, n] actions (a graph's own buffer, refreshed between replays), else the table's slice;
+        # device_policy: the fused launches draw their own actions (mgx_set_random_policy), nothing is read
+        if acts is None and not device_policy:
+            acts = actions[W + c * H:W + c * H + H]
         if compact:
             cbuf.carry_over()                            # every horizon starts a rollout (ring: no copy)
             if fused and E == H and args.gae_fused:      # one launch for the horizon, its GAE fused in
-                cbuf.rollout(0, actions[W + c * H:W + c * H + E], gae=dict(
+                cbuf.rollout(0, None if device_policy else acts[0:E], K=E, gae=dict(
                     values=vals, last_values=last_v, gamma=gamma, gae_lambda=lam, out=(adv, ret), stats=hist[c],
                     scratch=scratch))
             elif fused:                                  # one launch per refill epoch
                 for j in range(0, H, E):
-                    cbuf.rollout(j, actions[W + c * H + j:W + c * H + j + E])
+                    cbuf.rollout(j, None if device_policy else acts[j:j + E], K=E)
             else:
                 for j in range(H):
-                    cbuf.step(j, actions[W + c * H + j])
+                    cbuf.step(j, acts[j])
         else:
             for j in range(H):
-                eng.step_into(actions[W + c * H + j], reward=rew[j], done=dones[j])
+                eng.step_into(acts[j], reward=rew[j], done=dones[j])
         if not (fused and E == H and args.gae_fused):
             gae_dones(rew, vals, cbuf.dones if compact else dones, last_v, gamma, lam, stats=hist[c], scratch=scratch,
                       out=(adv, ret))                    # (ring: this horizon's block of start flags)
@@ -568,15 +578,38 @@ def measure_rollout(args, layout, world, rank, dev):
     if compact and args.graph:
         m = cbuf.blocks
         ng = -(-nchunks // m) * m
+    steps_since_reset = W
     if args.graph:
         # one hipGraph per horizon chunk (launch-bound loop -> one replay each); a chunk is whole
-        # refill epochs, so each graph holds its forks and joins (self-contained capture)
+        # refill epochs, so each graph holds its forks and joins (self-contained capture).
+        # FRESH ACTIONS EVERY REPLAY (round 6), uniform on {0..6}.  Rounds 2-5 replayed one fixed slice of actions in every replay,
+        # so env i repeated the same H actions forever: an env whose slice held 6-7 'done' actions consumed 6-7
+        # episodes per 20-step epoch, every epoch, against a production cap of ~3 -- its ring drained to the 2K
+        # floor within ~100 epochs and its wave then ran need-driven rounds (6-13) every epoch.  That, not the
+        # engine, was round 5's "steady-state drain" (tools/diag_ring_levels.py: fixed vs fresh actions).
+        # The draws: counter-based hashes whose counters live on the device (not torch's Philox: replay() would add two
+        # offset-fill launches and its bookkeeping before every graph launch, ~20 us of the 20-step window in the
+        # rocprofv3 trace, and a raw hipGraphLaunch would repeat them).  Fused layout: the rollout launches draw their
+        # own actions in the DMA wave that would have loaded them (mgx_set_random_policy) -- no kernel, no buffer, no
+        # action byte read.  A separate draw kernel beside the rollout and the refill measured ruinous (round 6: its
+        # 1,024 workgroups found slots only between theirs, lingered 120 us and slowed both by ~40 %).  Per-step
+        # layouts: mgx_random_actions redraws the graph's own buffer after its steps, on the steps' stream.
+        from mgx import random_actions
+        act_ctr = torch.zeros(2, dtype=torch.int64, device=dev)
+        act_seed = 4321 + rank
+        if fused:
+            eng.set_random_policy(act_seed)
+            abuf = [None] * ng
+        else:
+            abuf = [actions[W + (c % nchunks) * H:W + (c % nchunks) * H + H].clone() for c in range(ng)]
         s = torch.cuda.Stream(dev)
         with torch.cuda.stream(s):
             for c in range(ng):
                 gr = torch.cuda.CUDAGraph()
                 gr.capture_begin()
-                chunk(c % nchunks)
+                chunk(c % nchunks, abuf[c], device_policy=fused)
+                if not fused:                            # this graph's next actions, after its steps read them
+                    random_actions(abuf[c], act_ctr, seed=act_seed)
                 gr.capture_end()
                 graphs.append(gr)
         # one untimed replay of each graph (more warm-up steps: every graph is whole refill epochs
@@ -585,14 +618,18 @@ def measure_rollout(args, layout, world, rank, dev):
         for gr in graphs:
             gr.replay()
         torch.cuda.synchronize(dev)
-        # then whole cycles of untimed replays until the warm-up has kept the GPU busy for --warmup-ms: a few ms of
-        # warm-up left the first bench of a fresh process (kernel 8.9 vs 7.6 us per step) on a box whose
-        # clocks had not settled
-        while (time.perf_counter() - t_warm0) * 1e3 < args.warmup_ms:
-            for gr in graphs:
-                gr.replay()
+        steps_since_reset += ng * H
+        # then whole cycles of untimed replays (in cyclic order: each graph's actions are drawn by the one before
+        # it) until the rings have reached their steady state -- >= --steady-steps steps after mgx_reset (round 6:
+        # the timed region no longer sits in the first few hundred steps, when every ring is still nearly full) --
+        # and the GPU has been busy for --warmup-ms
+        while steps_since_reset < args.steady_steps or (time.perf_counter() - t_warm0) * 1e3 < args.warmup_ms:
+            for _ in range(16):
+                for gr in graphs:
+                    gr.replay()
+                steps_since_reset += ng * H
+                replay_cycles += 1
             torch.cuda.synchronize(dev)
-            replay_cycles += 1
     eng.clock_rewind()                                   # (the slots then hold the region's and the probe's launches)
     st0 = eng.stats()
     # refill launches inside the timed region: the forks the steps enqueued (captured once in the
@@ -610,6 +647,9 @@ def measure_rollout(args, layout, world, rank, dev):
     torch.cuda.synchronize(dev)
     from mgx.engine import graph_launch
     raw = args.graph_launch == "raw"
+    if args.mark_region and hasattr(torch.cuda, "_sleep"):
+        torch.cuda._sleep(1000)                          # trace marker (tools/trace_window.py): the region follows
+        torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
     for c in range(nchunks):
@@ -627,6 +667,9 @@ def measure_rollout(args, layout, world, rank, dev):
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    if args.mark_region and hasattr(torch.cuda, "_sleep"):
+        torch.cuda._sleep(1000)                          # trace marker: the region ended
+        torch.cuda.synchronize(dev)
     gpu_ms = ev0.elapsed_time(ev1)
     clk1 = (eng.clock_launches(0), eng.clock_launches(1), eng.clock_launches(2))
     timed_step_us = eng.clock_spans_us(0, clk0[0], clk1[0])      # the timed region's own kernel launches
@@ -710,37 +753,55 @@ def measure_rollout(args, layout, world, rank, dev):
     # untimed replays, then several timed replays.  The region above follows mgx_reset by a few hundred steps, when
     # every ring is still nearly full; over thousands of steps a few rings drain to the 2K floor and their waves
     # run need-driven rounds every epoch -- the slowest wave sets the refill launch.
+    # A second window much later (round 5: N = 1 only; round 6: every world size, barrier + max over ranks): the graphs
+    # replayed on, in cyclic order from where the region stopped, for --steady-ms more, then whole cycles timed.  The
+    # headline region itself already follows >= --steady-steps steps of warm-up; this checks that the line holds.
     steady = None
-    if graphs and world == 1 and args.steady_ms > 0 and layout == args.layout:
+    if graphs and args.steady_ms > 0 and layout == args.layout:
+        gi = nchunks % len(graphs)                       # the next graph in the cyclic order
         t_s = time.perf_counter()
         cyc = 0
         while (time.perf_counter() - t_s) * 1e3 < args.steady_ms:
-            for gr in graphs:
-                gr.replay()
+            for _ in range(len(graphs)):
+                graphs[gi].replay()
+                gi = (gi + 1) % len(graphs)
             torch.cuda.synchronize(dev)
             cyc += 1
-        reps = max(1, 200 // K)
+        nrep = len(graphs) * max(1, -(-200 // (len(graphs) * H)))   # whole cycles, >= 200 steps
         sa = eng.stats()
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize(dev)
         t0s = time.perf_counter()
-        for _ in range(reps):
-            for c in range(nchunks):
-                graphs[c].replay()
+        for k in range(nrep):
+            graphs[gi].replay()
+            if world > 1:
+                hist[gi % nchunks].copy_(_allreduce(hist[gi % nchunks], dist.ReduceOp.SUM))
+            gi = (gi + 1) % len(graphs)
         torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
         wall_s = time.perf_counter() - t0s
         sb = eng.stats()
-        prod_s = (sb["resets"] - sa["resets"]) + (sb["queued"] - sa["queued"])
-        cons_s = sb["resets"] - sa["resets"]
-        steady = {"value": n * K * reps / wall_s, "ms_per_step": wall_s * 1e3 / (K * reps),
-                  "timed_steps": K * reps, "after_steps": W + (replay_cycles + cyc) * len(graphs) * H + K,
+        tot = torch.tensor([wall_s, float((sb["resets"] - sa["resets"]) + (sb["queued"] - sa["queued"])),
+                            float(sb["resets"] - sa["resets"])], dtype=torch.float64, device=dev)
+        if world > 1:
+            wmax = _allreduce(tot[:1].clone(), dist.ReduceOp.MAX)
+            pc = _allreduce(tot[1:].clone(), dist.ReduceOp.SUM)
+            tot = torch.cat([wmax.to(dev), pc.to(dev)])
+        wall_s, prod_s, cons_s = float(tot[0]), float(tot[1]), float(tot[2])
+        steady = {"value": n * world * H * nrep / wall_s, "ms_per_step": wall_s * 1e3 / (H * nrep),
+                  "timed_steps": H * nrep,
+                  "after_steps": steps_since_reset + K + cyc * len(graphs) * H,
                   "produced_over_consumed": prod_s / max(cons_s, 1),
-                  "note": "the region's graphs replayed %d more cycles (%.0f ms) untimed, then %d times timed: the "
-                          "rings' steady state (a few hundred steps after mgx_reset they are still nearly full)"
-                          % (cyc, args.steady_ms, reps)}
+                  "ratio_to_value": None,
+                  "note": "the region's graphs replayed %d more cycles (%.0f ms) untimed, in cyclic order, then %d "
+                          "replays (whole cycles) timed, barrier + max over ranks" % (cyc, args.steady_ms, nrep)}
     if rank == 0:
         probe_s = (sum(probe_us) / len(probe_us)) * 1e-6 if probe_us else None
         resets_per_launch = (st1["resets"] - st0["resets"]) / K
-        b_alg = B_STEP * n + (3 * args.size ** 2 + 208) * resets_per_launch
+        dev_policy = fused and bool(graphs)              # the timed launches draw their own actions: no action byte
+        b_alg = (B_STEP - (1 if dev_policy else 0)) * n + (3 * args.size ** 2 + 208) * resets_per_launch
         gae_in = fused and E == H and args.gae_fused
         if gae_in:                                       # the launch also runs GAE over its steps: SURVEY 8(d)'s
             b_alg += 17 * n                              # 17 B per element (r, v, done, adv, ret), per step
@@ -802,19 +863,22 @@ def measure_rollout(args, layout, world, rank, dev):
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
-            "warmup": W + (replay_cycles * len(graphs) * H if graphs else 0),   # + the graphs' untimed replays
+            "warmup": steps_since_reset,                 # eager warm-up + the graphs' untimed replays
             "warmup_requested": args.warmup,
             "warmup_note": "warm-up raised to >= %d steps in whole refill epochs, then untimed replays of the "
-                           "graphs (%d cycles; --warmup-ms %.0f): every env starts its first episode at the "
-                           "reset, and the reset rate the timed window pays for (`window`) settles only after a few "
-                           "max_steps; the rings are still nearly full then (`steady_state`: thousands of steps "
-                           "later)" % (args.min_warmup, replay_cycles, args.warmup_ms),
+                           "graphs in cyclic order (%d cycles) until >= %d steps after mgx_reset (--steady-steps; "
+                           "--warmup-ms %.0f): the timed region sits in the rings' steady state, not in the first "
+                           "few hundred steps after the reset filled every ring; every replay draws fresh random "
+                           "actions for the next one" % (args.min_warmup, replay_cycles, args.steady_steps,
+                                                         args.warmup_ms),
+            "steps_after_reset": steps_since_reset,
             "ms_per_step": wall_max * 1e3 / K,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (uniform random actions on {0..6}, seed 1234+rank; env i seeded 42+i; "
+            "data": "synthetic (uniform random actions on {0..6}: seed 1234+rank for the eager warm-up, then drawn "
+                    "afresh inside the graphs at every replay (mgx_random_actions, seed 4321+rank); env i seeded 42+i; "
                     "synthetic values for GAE)",
             "config": {"workload": _workload_name(args, mission, n, world) + (
                            " [fused rollout: one launch per %d-step refill epoch, observation rows into the rollout "
@@ -877,7 +941,8 @@ def measure_rollout(args, layout, world, rank, dev):
                          "stack_bytes_per_launch": stack_bytes,
                          "achieved_incl_stack": (b_alg + stack_bytes) / per_launch_s / 1e9},
             "gae": {"horizon": gae_h, "T1024": gae_1k},
-            "steady_state": steady,
+            "steady_state": dict(steady, ratio_to_value=steady["value"] / (total_env_steps / wall_max))
+                            if steady else None,
             "gpu_time_ms": gpu_max * 1e3,
         }
         return out

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MGX_ABI_VERSION 6
+#define MGX_ABI_VERSION 7
 
 /* Live-lock cap (engine policy; the reference hangs): a
  * reset attempt may consume at most this many MT19937 words; the attempt that
@@ -92,10 +92,10 @@ typedef struct mgx_config {
                                   power of two of 10-word groups, >= 5,120).  The stream is extended on the
                                   device as cursors advance -- no lifetime limit; only the spread between
                                   the oldest live cursor and the newest must stay below it */
-    int32_t ring_depth;        /* pre-generated episodes per env (0 -> 256; rounded up to a power of two
+    int32_t ring_depth;        /* pre-generated episodes per env (0 -> 512 since ABI 7, 256 before; rounded up to a power of two
                                   <= 4096, ring positions are mod 2^16; -1 = no ring: every auto-reset
                                   generated inline) */
-    int32_t refill_every;      /* steps per refill epoch K (0 -> ring_depth/4; clamped to <= ring_depth/2:
+    int32_t refill_every;      /* steps per refill epoch K (0 -> min(ring_depth/4, 64); clamped to <= ring_depth/2:
                                   each epoch keeps >= K queued, and a step pops <= 1 episode) */
     double percent_obstacles;  /* `env.percent_obstacles` (single.yaml:28: 0.05); used when obstacles */
     int32_t manual;            /* PlaygroundEnv(manual=True) (make_env(manual=True), environment.py:10-20):
@@ -141,8 +141,8 @@ mgx_status mgx_destroy(mgx_handle *h);
  * calls follow SB3: seeded (PCG64 only) if mgx_set_seed was called since the
  * last reset, else unseeded; both streams continue from each env's current
  * episode, and mission_done / the stored reward persist.
- * It also pre-generates ring_depth episodes per env (on `stream`; ~13 ms at
- * 65,536 envs, S = 8).  `livelock_dev` (optional i32 [N]). */
+ * It also pre-generates ring_depth episodes per env (on `stream`; ~26 ms at
+ * 65,536 envs, S = 8, D = 512).  `livelock_dev` (optional i32 [N]). */
 mgx_status mgx_reset(mgx_handle *h, const mgx_obs *obs, int32_t *livelock_dev, void *stream);
 
 /* VecEnv.seed(seed) (SB3): the NEXT mgx_reset seeds env i's PCG64 with
@@ -324,6 +324,27 @@ mgx_status mgx_poll_error(mgx_handle *h, void *stream, uint32_t *bits);
  * [7] MT19937 words generated so far (the device ring holds the last mt_table_words of them).
  * Synchronises `stream` and the refill stream. */
 mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]);
+
+/* The fused rollout's own random policy (ABI 7): once set, mgx_rollout_compact[_gae] may be called with
+ * actions_dev = NULL, and each launch then draws its K x N actions on the device, in the DMA wave that would have
+ * loaded them -- exactly mgx_random_actions' draws (n_actions 7) over a [K][N] buffer at counter c = the number of
+ * such launches since this call (no actions buffer, nothing read).  enable = 0 turns it off.  Synchronises. */
+mgx_status mgx_set_random_policy(mgx_handle *h, int enable, uint64_t seed);
+
+/* Synthetic random policy (ABI 7; env.action_space.sample() for a whole batch -- the benchmark's random-action
+ * rollouts, a random agent's evaluation): out_dev i32 [count] = uniform draws on {0 .. n_actions-1}
+ * (1 <= n_actions <= 65536) from a counter-based hash of (seed, counter, i): key = splitmix64(seed + c *
+ * 0x9E3779B97F4A7C15), h = splitmix64(key ^ (i * 0xD1B54A32D192ED03)), out = ((h >> 32) * n_actions) >> 32
+ * (mod 2^64; c = counter_dev[0]).  The launch then advances counter_dev[0] by one on the device, so the same launch
+ * captured in a hipGraph draws fresh actions at every replay.  counter_dev: u64 [2], caller-owned, zeroed before
+ * the first use (word 1 is the launch's own workgroup tally; launches sharing a counter must not overlap). */
+mgx_status mgx_random_actions(int32_t *out_dev, int64_t count, int n_actions, uint64_t seed, uint64_t *counter_dev,
+                              void *stream);
+
+/* Diagnostics (ABI 7): the episodes queued in each env's ring now, (tail - head) mod 2^16, into a HOST
+ * array levels[N] (what mgx_stats [4] sums).  Synchronises `stream` and the refill stream.  Measurement
+ * only, no reference counterpart (tools/diag_ring_levels.py: the ring-level distribution over long runs). */
+mgx_status mgx_ring_levels(mgx_handle *h, void *stream, uint16_t *levels);
 
 /* Diagnostics: the first n (<= 32) raw device counters (phase / section clocks of
  * -DMGX_STAMPS / -DMGX_GEN_STAMPS builds; zero otherwise).  Synchronises. */

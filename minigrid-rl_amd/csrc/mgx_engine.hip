@@ -162,6 +162,10 @@ struct KParams {
     uint4 *start_rng;       // [N][2] inline mode only: RNG state at the start of the current episode's
                             //        generation (mgx_scene regenerates it), else null
     KClock clk;             // mgx_set_clock: kernel clocks (clk.slots == 0: off)
+    // mgx_set_random_policy (ABI 7): the fused rollout draws its own actions when launched without any --
+    // rnd_ctr[b] = random-policy launches rollout workgroup b has run (its sole writer); null: off
+    unsigned long long *rnd_ctr;
+    uint64_t rnd_seed;
 };
 
 __device__ __forceinline__ unsigned long long clk_now() { return (unsigned long long)wall_clock64(); }
@@ -1293,6 +1297,22 @@ __global__ __launch_bounds__(BLOCK_THREADS, 4) void mgx_step_kernel(KParams p, K
 // back once, at the end.  The refill may run concurrently (it reads ring_head once, at its start:
 // a stale head only under-estimates its free slots); the K steps lie within one refill epoch, whose
 // join published >= K episodes per env, so every staged slot is in [head, pub).
+// ---- the synthetic random policy's draws (mgx_random_actions, mgx_set_random_policy; include/mgx.h): action i of
+// launch c = Lemire's multiply-shift of the high half of splitmix64(key_c ^ i * M), key_c = splitmix64(seed + c * G)
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t rnd_key(uint64_t seed, unsigned long long c) {
+    return splitmix64(seed + (uint64_t)c * 0x9E3779B97F4A7C15ull);
+}
+__device__ __forceinline__ int32_t rnd_draw(uint64_t key, uint64_t i, uint32_t n_actions) {
+    const uint64_t h = splitmix64(key ^ (i * 0xD1B54A32D192ED03ull));
+    return (int32_t)(((h >> 32) * (uint64_t)n_actions) >> 32);
+}
+
 struct ROut {
     uint8_t *rows, *mids, *t_rows;   // [K][N][148], [K][N], [N][148]
     float *reward;                   // [K][N]
@@ -1399,8 +1419,19 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
         }
     };
     rpos_t head0 = 0;                                // the DMA wave: this env's ring head at the launch's start
+    // random policy (no actions buffer, mgx_set_random_policy): the DMA wave draws step t's actions itself, the
+    // draws of mgx_random_actions over a [K][N] buffer at this launch's counter (the workgroup's own: every
+    // workgroup runs every launch, so all of them hold the same count)
+    const bool rnd = actions == nullptr;
+    uint64_t rkey = 0;
+    unsigned long long rc = 0;
+    if (rnd && dmaw) {
+        rc = *reinterpret_cast<volatile const unsigned long long *>(p.rnd_ctr + blockIdx.x);
+        rkey = rnd_key(p.rnd_seed, rc);
+    }
     if (dmaw && lane < ne) {
-        __builtin_amdgcn_global_load_lds(actions + e0 + lane, s_act, 4, 0, 0);
+        if (rnd) s_act[lane] = rnd_draw(rkey, (uint64_t)(e0 + lane), 7u);
+        else __builtin_amdgcn_global_load_lds(actions + e0 + lane, s_act, 4, 0, 0);
         // the end of the env's published episodes: ring_pubn, read ONCE (the slide after a refill running
         // beside this launch may raise it meanwhile; every value it takes is a completed refill's), shared
         // with the step wave through s_pub so that the staging and the pops agree
@@ -1444,9 +1475,13 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
             // (LDS-DMA only: a register load here would make the wave wait for it -- and for every
             // prefetch in flight -- before the post-logic barrier, the whole block with it)
             if (lanev < ne) {
-                if (t + 1 < K)
-                    __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lanev, s_act + (tb ^ 1) * EPB,
-                                                     4, 0, 0);
+                if (t + 1 < K) {
+                    if (rnd)
+                        s_act[(tb ^ 1) * EPB + lanev] = rnd_draw(rkey, (uint64_t)(t + 1) * (uint64_t)N + (uint64_t)(e0 + lanev), 7u);
+                    else
+                        __builtin_amdgcn_global_load_lds(actions + (int64_t)(t + 1) * N + e0 + lanev,
+                                                         s_act + (tb ^ 1) * EPB, 4, 0, 0);
+                }
                 const uint32_t nh = s_nh[tb ^ 1][lanev];
                 if (nh != NO_POP && (rpos_t)(s_pub[lanev] - nh) > 1) stage((rpos_t)(nh + 1));
             }
@@ -1735,6 +1770,7 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
             dst[i] = *reinterpret_cast<const uint4 *>(s_grid + c * (EPB * 16) + le * 16);
         }
     }
+    if (rnd && tid == RT) p.rnd_ctr[blockIdx.x] = rc + 1ull;   // (a lane of the DMA wave: a vector store)
     if (tid == 0) {
         const int sb = (int)(blockIdx.x / (64 / EPB));   // the stats slot of these 64 envs (32-env blocks: two)
         atomicAdd(&p.blk[sb].x, (unsigned long long)ne * (unsigned long long)K);
@@ -2397,6 +2433,33 @@ __global__ __launch_bounds__(GAE_SHARDS) void mgx_gae_reduce_kernel(double *__re
     }
 }
 
+// ==================================================== synthetic random policy
+// mgx_random_actions: out[i] = uniform on {0 .. n_actions - 1} from a counter-based hash of (seed, launch counter, i)
+// -- splitmix64 twice, then Lemire's multiply-shift of the high 32 bits (bias < n / 2^32) -- so that a launch
+// captured once in a hipGraph draws fresh actions at every replay: the counter lives in device memory and the last
+// workgroup to finish advances it (every workgroup has read it by then: each reads it before its own tally add).
+// Integer hashing, coalesced dword stores: 4 B written per action (HBM-bound, ~1 us per 10^6 actions).
+__global__ __launch_bounds__(256) void mgx_random_actions_kernel(int32_t *__restrict__ out, int64_t count,
+                                                                  uint32_t n_actions, uint64_t seed,
+                                                                  unsigned long long *ctr) {
+    const unsigned long long c = *reinterpret_cast<volatile unsigned long long *>(ctr);
+    const uint64_t key = splitmix64(seed + (uint64_t)c * 0x9E3779B97F4A7C15ull);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        const uint64_t h = splitmix64(key ^ ((uint64_t)i * 0xD1B54A32D192ED03ull));
+        out[i] = (int32_t)(((h >> 32) * (uint64_t)n_actions) >> 32);
+    }
+    __syncthreads();                                   // every thread of this workgroup has read the counter
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(reinterpret_cast<unsigned int *>(ctr + 1), 1u) == gridDim.x - 1) {
+            *reinterpret_cast<volatile unsigned long long *>(ctr) = c + 1ull;   // (vector store)
+            *reinterpret_cast<volatile unsigned int *>(ctr + 1) = 0u;
+            __threadfence();
+        }
+    }
+}
+
 // ========================================================= compact layout kernels
 // mgx_observe_compact: the current observation of every env as a compact row (byte 0
 // direction, bytes 1..147 the [c][vx][vy] frame) + mission id -- e.g. right after mgx_reset,
@@ -2664,7 +2727,7 @@ struct mgx_handle {
                             // (round 2: the all-problems kernel measured the same speed)
     hipStream_t side;       // refill stream
     hipEvent_t ev_fork, ev_done;
-    void *allocs[17];
+    void *allocs[18];       // [17]: mgx_set_random_policy's per-workgroup launch counters
     uint32_t *scene_dev;    // mgx_scene's record (inside allocs[15], inline mode only)
 };
 
@@ -2746,10 +2809,14 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     h->cfg = *cfg;
     h->device = device;
     if (h->cfg.livelock_words <= 0) h->cfg.livelock_words = MGX_LIVELOCK_WORDS;
-    // default depth 256 (round 3; 128 before): at refill epochs of D/4 = 64 steps the lanes' deficits
-    // (production follows the wave's mean consumption, capped at the grid's) stay far from the invariant's
-    // 2K, so need-driven attempt rounds do not set the launch
-    if (h->cfg.ring_depth == 0) h->cfg.ring_depth = 256;
+    // default depth 512 (round 6; 256 since round 3, 128 before).  A lane's ring level is a random walk
+    // (consumption i.i.d. per epoch, variance ~ its mean) reflected at D, with the drift the production ceiling
+    // gives it (mgx_mt_slide_kernel: mean x (1 + 9 / (D - 2K)), 18 e-folds of the walk's tail between D and
+    // the invariant's floor 2K).  At D = 256 and the driver's 20-step epochs that target is 3.04 episodes per
+    // epoch: one epoch in ~28 ran a fourth attempt round (the launch +33 %).  At D = 512 it is 2.97 -- three
+    // rounds every epoch, with 22 e-folds of the tail at the integer rounding's own drift.  4.3 GB of rings at
+    // 65,536 envs (S = 8), 21 GB at config 5's 131,072 x 16 x 16 (288 GB of HBM)
+    if (h->cfg.ring_depth == 0) h->cfg.ring_depth = 512;
     if (h->cfg.ring_depth < 0) {
         h->cfg.ring_depth = 0;                                   // ring disabled: every reset generated inline
     } else {
@@ -2757,7 +2824,7 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         while (d < h->cfg.ring_depth && d < MGX_MAX_RING) d <<= 1;   // power of two (mod-2^16 ring indices)
         h->cfg.ring_depth = d;
     }
-    if (h->cfg.refill_every <= 0) h->cfg.refill_every = std::max(1, h->cfg.ring_depth / 4);
+    if (h->cfg.refill_every <= 0) h->cfg.refill_every = std::max(1, std::min(h->cfg.ring_depth / 4, 64));
     if (h->cfg.refill_every > h->cfg.ring_depth / 2) h->cfg.refill_every = std::max(1, h->cfg.ring_depth / 2);
     // default production cap: ~1.3x a random policy's consumption (1 in 7 steps ends an episode on
     // 'done' alone; 0.146 resets per env-step measured at config 2), i.e. 6 at the default epoch of 32
@@ -2942,6 +3009,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     }
     p.D = D;
     p.start_rng = nullptr;
+    p.rnd_ctr = nullptr;                   // random policy off (mgx_set_random_policy)
+    p.rnd_seed = 0;
     if (D == 0) {   // inline mode: keep each episode's generation start state (mgx_scene) + its record
         const size_t bytes = (size_t)N * 32 + MGX_SCENE_WORDS * sizeof(uint32_t);
         hipError_t e = hipMalloc(&h->allocs[15], bytes);
@@ -3347,7 +3416,9 @@ mgx_status mgx_step_compact(mgx_handle *h, const void *actions_dev, int action_b
 static double *gae_scratch(double *stats_scratch_dev);
 static mgx_status rollout_impl(mgx_handle *h, const int32_t *actions_dev, int K, const mgx_rollout_out *out,
                                const mgx_gae_args *gae, void *stream) {
-    if (!h || !out || !actions_dev) return fail(MGX_ERR_INVALID, "mgx_rollout_compact: null argument");
+    if (!h || !out) return fail(MGX_ERR_INVALID, "mgx_rollout_compact: null argument");
+    if (!actions_dev && !h->kp.rnd_ctr)
+        return fail(MGX_ERR_INVALID, "mgx_rollout_compact: null actions_dev (and no mgx_set_random_policy)");
     if (!out->rows_dev || !out->mission_ids_dev || !out->rewards_dev || !out->terminated_dev || !out->truncated_dev ||
         !out->dones_dev)
         return fail(MGX_ERR_INVALID, "mgx_rollout_compact: missing output buffer");
@@ -3519,6 +3590,33 @@ static double *gae_scratch(double *stats_scratch_dev) {
     return static_cast<double *>(p);
 }
 
+mgx_status mgx_set_random_policy(mgx_handle *h, int enable, uint64_t seed) {
+    if (!h) return fail(MGX_ERR_INVALID, "null handle");
+    (void)hipSetDevice(h->device);
+    if (!enable) {
+        h->kp.rnd_ctr = nullptr;
+        return MGX_OK;
+    }
+    const size_t words = (size_t)((h->kp.n + 31) / 32) + 1;   // one per rollout workgroup (32- or 64-env blocks)
+    if (!h->allocs[17]) HIP_TRY(hipMalloc(&h->allocs[17], words * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(h->allocs[17], 0, words * sizeof(unsigned long long)));
+    HIP_TRY(hipDeviceSynchronize());
+    h->kp.rnd_ctr = (unsigned long long *)h->allocs[17];
+    h->kp.rnd_seed = seed;
+    return MGX_OK;
+}
+
+mgx_status mgx_random_actions(int32_t *out_dev, int64_t count, int n_actions, uint64_t seed, uint64_t *counter_dev,
+                              void *stream) {
+    if (!out_dev || !counter_dev || count <= 0 || n_actions < 1 || n_actions > 65536)
+        return fail(MGX_ERR_INVALID, "mgx_random_actions: bad argument");
+    const int64_t blocks = std::min<int64_t>((count + 1023) / 1024, 1024);
+    hipLaunchKernelGGL(mgx_random_actions_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, out_dev,
+                       count, (uint32_t)n_actions, seed, (unsigned long long *)counter_dev);
+    HIP_TRY(hipGetLastError());
+    return MGX_OK;
+}
+
 mgx_status mgx_gae(const float *rewards_dev, const float *values_dev, const float *episode_starts_dev,
                    const float *last_values_dev, const uint8_t *last_dones_dev, int64_t T, int64_t N, float gamma,
                    float gamma_lambda, float *advantages_dev, float *returns_dev, double *adv_stats_dev,
@@ -3600,6 +3698,21 @@ mgx_status mgx_stats(mgx_handle *h, void *stream, uint64_t out[8]) {
         c[7] = m.hi * (uint64_t)MT_FIELDS;
     }
     for (int i = 0; i < 8; i++) out[i] = c[i];
+    return MGX_OK;
+}
+
+mgx_status mgx_ring_levels(mgx_handle *h, void *stream, uint16_t *levels) {
+    if (!h || !levels) return fail(MGX_ERR_INVALID, "null argument");
+    HIP_TRY(hipStreamSynchronize(h->side));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    const int64_t N = h->kp.n;
+    if (h->kp.D <= 0) {
+        std::memset(levels, 0, (size_t)N * sizeof(uint16_t));
+        return MGX_OK;
+    }
+    std::vector<rpos_t> ht((size_t)2 * N);
+    HIP_TRY(hipMemcpy(ht.data(), h->kp.ring_head, ht.size() * sizeof(rpos_t), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < N; i++) levels[i] = (rpos_t)(ht[(size_t)(N + i)] - ht[(size_t)i]);
     return MGX_OK;
 }
 

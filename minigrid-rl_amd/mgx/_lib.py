@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("MGX_LIB_PATH", os.path.join(HERE, "libmgx.so"))   # o
 
 MGX_OK = 0
 GAE_SCRATCH_WORDS = 512  # == MGX_GAE_SCRATCH_WORDS (include/mgx.h)
-ABI_VERSION = 6        # == MGX_ABI_VERSION (include/mgx.h)
+ABI_VERSION = 7        # == MGX_ABI_VERSION (include/mgx.h)
 PROBLEMS = {"multi": 0, "full": 1, "gto": 2, "gtg": 3, "opn": 4, "pkp": 5, "drp": 6, "mov": 7}
 TERMINAL = {"none": 0, "truncated": 1, "all": 2}
 DEVERR = {1: "MT19937 ring: a cursor left the window of the stream the device holds", 2: "action outside 0..6 (ValueError: Unknown action)",
@@ -26,7 +26,8 @@ DEVERR = {1: "MT19937 ring: a cursor left the window of the stream the device ho
 EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mgx_reset", "mgx_step",
            "mgx_join", "mgx_get_config", "mgx_set_seed", "mgx_gae", "mgx_gae_dones", "mgx_poll_error", "mgx_stats", "mgx_debug_counters", "mgx_dump_state", "mgx_mission_text",
            "mgx_step_compact", "mgx_rollout_compact", "mgx_rollout_compact_gae", "mgx_observe_compact", "mgx_gather",
-           "mgx_gather_ring", "mgx_scene", "mgx_set_clock", "mgx_clock_words", "mgx_clock_groups")
+           "mgx_gather_ring", "mgx_scene", "mgx_set_clock", "mgx_clock_words", "mgx_clock_groups",
+           "mgx_ring_levels", "mgx_random_actions", "mgx_set_random_policy")
 CLOCK_CLASSES = 3   # == MGX_CLOCK_CLASSES (include/mgx.h)
 
 
@@ -113,6 +114,9 @@ def load():
     L.mgx_gae_dones.argtypes = [P, P, P, P, I64, I64, ctypes.c_float, ctypes.c_float, P, P, P, P, P]
     L.mgx_poll_error.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]
     L.mgx_stats.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64)]
+    L.mgx_ring_levels.argtypes = [P, P, P]
+    L.mgx_random_actions.argtypes = [P, I64, I, ctypes.c_uint64, P, P]
+    L.mgx_set_random_policy.argtypes = [P, I, ctypes.c_uint64]
     L.mgx_debug_counters.argtypes = [P, P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.mgx_dump_state.argtypes = [P, P] + [P] * 10
     L.mgx_mission_text.argtypes = [I, ctypes.c_char_p, ctypes.c_size_t]

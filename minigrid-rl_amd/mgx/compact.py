@@ -112,19 +112,26 @@ class CompactBuffer:
                    "mgx_step_compact")
         e.calls += 1
 
-    def rollout(self, t, actions, gae=None):
+    def rollout(self, t, actions, gae=None, K=None):
         """K = len(actions) steps in ONE launch (mgx_rollout_compact): actions int32 [K, N] known up
-        front (a random-action or scripted rollout); observations t+1 .. t+K, rewards / dones of
+        front (a random-action or scripted rollout) -- or None with `K` given, after
+        engine.set_random_policy(seed): the launch draws its own uniform actions on the device
+        (mgx_random_actions' draws at the engine's random-launch counter); observations t+1 .. t+K, rewards / dones of
         steps t .. t+K-1 -- the same as K step() calls, bit for bit.  The K steps must lie within one
         refill epoch of the engine.
         gae: dict(values f32 [K, N], last_values f32 [N], gamma, gae_lambda, out=(adv, ret) f32 [K, N],
         stats=f64 [3] or None, scratch=None) -- also the GAE of these K steps, fused into the launch
         (mgx_rollout_compact_gae): gae_dones(rewards[t:t+K], values, dones of the K steps, ...) bit for bit."""
         e = self.engine
-        K = int(actions.shape[0])
-        if actions.device != e.device or actions.dtype != torch.int32 or tuple(actions.shape) != (K, self.N) \
-                or not actions.is_contiguous():
-            raise ValueError("actions must be a contiguous int32 [K, %d] tensor on %s" % (self.N, e.device))
+        if actions is None:
+            if getattr(e, "random_policy", None) is None or K is None:
+                raise ValueError("rollout without actions needs engine.set_random_policy(seed) and K")
+            K = int(K)
+        else:
+            K = int(actions.shape[0])
+            if actions.device != e.device or actions.dtype != torch.int32 or tuple(actions.shape) != (K, self.N) \
+                    or not actions.is_contiguous():
+                raise ValueError("actions must be a contiguous int32 [K, %d] tensor on %s" % (self.N, e.device))
         if t < 0 or t + K > self.T:
             raise ValueError("steps %d..%d outside the buffer's %d" % (t, t + K - 1, self.T))
         r = self.row(t + 1)
@@ -167,6 +174,8 @@ class CompactBuffer:
             _lib.check(e.L.mgx_rollout_compact_gae(e.h, _ptr(actions), K, ctypes.byref(o), ctypes.byref(g),
                                                    e._stream()), "mgx_rollout_compact_gae")
         e.calls += K
+        if actions is None:
+            e.random_launches += 1
 
     def carry_over(self):
         """Start the next rollout: its history rows and observation 0 are this one's last rows (ring: read in

@@ -219,6 +219,23 @@ class MgxEngine:
         return dict(steps=int(out[0]), resets=int(out[1]), livelocks=int(out[2]), max_mt_cursor=int(out[3]),
                     queued=int(out[4]), refill_launches=int(out[5]), calls=int(out[6]), mt_generated=int(out[7]))
 
+    def set_random_policy(self, seed=0, enable=True):
+        """The fused rollout's own random policy (mgx_set_random_policy): CompactBuffer.rollout(t, None) then draws
+        each launch's [K, N] actions on the device -- mgx_random_actions' draws at counter c = the launches since
+        this call (`random_launches` counts them on the host)."""
+        _lib.check(self.L.mgx_set_random_policy(self.h, 1 if enable else 0, ctypes.c_uint64(seed & (2 ** 64 - 1))),
+                   "mgx_set_random_policy")
+        self.random_policy = (seed & (2 ** 64 - 1)) if enable else None
+        self.random_launches = 0
+
+    def ring_levels(self):
+        """Episodes queued in each env's ring now (mgx_ring_levels: (tail - head) mod 2^16), a numpy u16 [N]
+        (synchronises; measurement only)."""
+        import numpy as np
+        out = np.zeros(self.n, np.uint16)
+        _lib.check(self.L.mgx_ring_levels(self.h, self._stream(), out.ctypes.data_as(_P)), "mgx_ring_levels")
+        return out
+
     def debug_counters(self, n=32):
         """Raw diagnostic counters (section clocks of the stamp builds)."""
         out = (ctypes.c_uint64 * n)()
@@ -352,6 +369,21 @@ def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lam
                          ctypes.c_float(gamma), ctypes.c_float(gl), _ptr(adv), _ptr(ret), _ptr(stats),
                          _ptr(_scratch_for(stats, scratch)), stream), "mgx_gae")
     return adv, ret
+
+
+def random_actions(out, counter, seed=0, n_actions=7):
+    """A random policy's actions for a whole batch (libmgx mgx_random_actions): fills the contiguous int32 device
+    tensor `out` with uniform draws on {0..n_actions-1} from a counter-based hash of (seed, counter[0], index), then
+    advances counter[0] by one ON THE DEVICE -- the launch can be captured in a hipGraph and draws fresh actions at
+    every replay (no host bookkeeping, unlike torch's Philox offsets).  `counter`: a zeroed int64 device tensor of 2
+    words, one per stream of launches that must not overlap.  Host restatement: oracle.random_actions_ref."""
+    L = _lib.load()
+    assert out.dtype == torch.int32 and out.is_contiguous() and out.is_cuda
+    assert counter.dtype == torch.int64 and counter.numel() >= 2 and counter.device == out.device
+    stream = ctypes.c_void_p(torch.cuda.current_stream(out.device).cuda_stream)
+    _lib.check(L.mgx_random_actions(_ptr(out), out.numel(), int(n_actions), ctypes.c_uint64(seed & (2 ** 64 - 1)),
+                                    _ptr(counter), stream), "mgx_random_actions")
+    return out
 
 
 def gae_dones(rewards, values, dones, last_values, gamma, gae_lambda, stats=None, out=None, scratch=None):

@@ -224,3 +224,22 @@ def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lam
         adv[t] = last
     ret = (adv + values).astype(np.float32)
     return adv, ret
+
+
+def _splitmix64(x):
+    """splitmix64 over a numpy uint64 array (mod 2^64)."""
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def random_actions_ref(count, seed, counter, n_actions=7):
+    """Restatement of mgx_random_actions (include/mgx.h, ABI 7): the synthetic random policy's actions of the launch
+    that reads counter value `counter` -- no reference counterpart beyond env.action_space.sample() (uniform)."""
+    with np.errstate(over="ignore"):
+        key = _splitmix64(np.uint64(seed) + np.uint64(counter) * np.uint64(0x9E3779B97F4A7C15))
+        i = np.arange(count, dtype=np.uint64)
+        h = _splitmix64(key ^ (i * np.uint64(0xD1B54A32D192ED03)))
+        return (((h >> np.uint64(32)) * np.uint64(n_actions)) >> np.uint64(32)).astype(np.int32)

@@ -1,0 +1,94 @@
+"""Ring levels and refill cost over a long run at the driver's shape (config 2: GTG 8x8, 65,536 envs, 20-step
+refill epochs, one fused rollout graph per ring block, replayed in turn as bench.py does).
+
+ACTIONS=fixed  every replay of a graph reads the same 20 action rows (bench.py rounds 2-5): env i repeats one
+               20-action sequence forever, so its consumption per epoch is persistent -- an env whose sequence
+               holds 6-7 'done' actions pops 6-7 episodes every epoch against a production of ~3.
+ACTIONS=fresh  each graph redraws the next graph's actions on a branch of its own (bench.py round 6), so every
+               env's consumption is i.i.d. from epoch to epoch, as in a random-action rollout.
+
+Per window of 1,000 steps (one JSON line): queued episodes per env (mean, 1st percentile, min), envs below the
+invariant's 2K floor, resets per env per epoch, produced / consumed, the refill's and the rollout's device-clock
+spans per launch (mean, max), and the window's env-steps/s (host wall clock).  Product library (no diagnostic
+build): the levels come from mgx_ring_levels (ABI 7)."""
+import json
+import os
+import sys
+import time
+
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "minigrid-rl_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mgx import MgxEngine  # noqa: E402
+from mgx.compact import CompactBuffer  # noqa: E402
+
+n = int(os.environ.get("N_ENVS", 65536))
+E = int(os.environ.get("REFILL_EVERY", 20))
+mode = os.environ.get("ACTIONS", "fresh")
+windows = int(os.environ.get("WINDOWS", 20))
+wsteps = int(os.environ.get("WINDOW_STEPS", 1000)) // (2 * E) * (2 * E)
+dev = torch.device("cuda", 0)
+eng = MgxEngine(problem="multi", mission=int(os.environ.get("MISSION", 5)), size=8, num_objects=4, n_envs=n,
+                terminal_mode="truncated", refill_every=E, device=dev)
+per_window = wsteps // E
+eng.enable_clock(slots=per_window + 8)
+cbuf = CompactBuffer(eng, E, ring=True)
+g = torch.Generator(device=dev)
+g.manual_seed(1234)
+warm = torch.randint(0, 7, (256, n), device=dev, generator=g, dtype=torch.int32)
+eng.reset()
+cbuf.observe(0)
+for t in range(0, 256 - 256 % E, E):
+    cbuf.carry_over()
+    cbuf.rollout(0, warm[t:t + E])
+eng.join()
+torch.cuda.synchronize(dev)
+steps = (256 // E) * E
+ng = cbuf.blocks
+torch.cuda.default_generators[0].manual_seed(4321)
+abuf = [torch.randint(0, 7, (E, n), device=dev, generator=g, dtype=torch.int32) for _ in range(ng)]
+graphs = []
+s, s_act = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+with torch.cuda.stream(s):
+    for c in range(ng):
+        gr = torch.cuda.CUDAGraph()
+        gr.capture_begin()
+        if mode == "fresh":
+            s_act.wait_stream(s)
+            with torch.cuda.stream(s_act):
+                abuf[(c + 1) % ng].random_(0, 7)
+        cbuf.carry_over()
+        cbuf.rollout(0, abuf[c])
+        eng.join()
+        if mode == "fresh":
+            s.wait_stream(s_act)
+        gr.capture_end()
+        graphs.append(gr)
+for gr in graphs:
+    gr.replay()
+steps += ng * E
+torch.cuda.synchronize(dev)
+K2 = 2 * E
+for w in range(windows):
+    eng.clock_rewind()
+    s0 = eng.stats()
+    t0 = time.perf_counter()
+    for k in range(per_window):
+        graphs[k % ng].replay()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    s1 = eng.stats()
+    steps += per_window * E
+    refill = eng.clock_spans_us(1, 0, per_window)
+    roll = eng.clock_spans_us(0, 0, per_window)
+    lv = eng.ring_levels().astype(np.int64)
+    cons = s1["resets"] - s0["resets"]
+    prod = cons + s1["queued"] - s0["queued"]
+    print(json.dumps(dict(
+        actions=mode, window=w, steps_after_reset=steps, level_mean=float(lv.mean()),
+        level_p1=float(np.percentile(lv, 1)), level_min=int(lv.min()), envs_below_2K=int((lv < K2).sum()),
+        resets_per_env_epoch=cons / n / per_window, produced_over_consumed=prod / max(cons, 1),
+        refill_us_mean=float(np.mean(refill)), refill_us_max=float(np.max(refill)),
+        rollout_us_per_step=float(np.mean(roll)) / E, env_steps_per_s=n * per_window * E / wall)), flush=True)
+eng.poll_error()
