@@ -45,6 +45,7 @@ mgx_gae_dones alone at the horizon and at T=1024 (17 B per element).
   `--horizon` env steps + n_epochs of minibatch training); value = env-steps/s.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -113,6 +114,9 @@ def parse():
                     help="timed graph replays: torch's CUDAGraph.replay(), or hipGraphLaunch on the graph exec "
                          "(mgx.engine.graph_launch: without replay()'s ~9 us of host bookkeeping; round 5 A/B: "
                          "no difference on the driver's line, 6.04-6.18 vs 5.95-6.23 x 10^9)")
+    ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
+                    help="fused layout, one launch per horizon: each timed chunk as a captured hipGraph replay, or as "
+                         "ONE prepared C call (rollout + refill fork + GAE, ctypes arguments built once) + mgx_join")
     ap.add_argument("--mark-region", type=int, default=0,
                     help="a torch.cuda._sleep kernel right before and after the timed region (kernel-trace marker for "
                          "tools/trace_window.py; outside the region)")
@@ -196,6 +200,12 @@ def cpu_baseline(args, seconds):
                 cap_note="P = min(affinity, 16): the reference's SubprocVecEnv runs n_envs = 16 workers "
                          "(algorithm/ppo.yaml:4), and a shared GPU box grants 16 CPUs per GPU",
                 reference_python=_reference_cpu(),
+                # every logical CPU of the host: not run -- a GPU box grants one GPU's job 16 CPUs and
+                # asks that worker pools stay within that share -- so priced from the measured per-process rate (the
+                # P processes run one env each, independently: the rate scales with processes up to the share)
+                all_affinity_extrapolated={"value": all_cores / P * affinity, "processes": affinity,
+                                           "note": "measured per-process rate x %d logical CPUs; NOT measured (the "
+                                                   "box's CPU share is 16)" % affinity},
                 legs={"all_cores": {"value": all_cores, "processes": P, "envs_per_process": 1},
                       "one_thread": {"value": s1 / t1, "processes": 1, "envs": 1024, "seconds": t1},
                       "config1_gtg8_1env": {"value": c1 / tc1, "processes": 1, "envs": 1, "seconds": tc1}})
@@ -413,6 +423,21 @@ def _profile_dir():
     return None, sha
 
 
+class _PreparedChunk:
+    """--launch eager: one horizon chunk as a prepared C call + its join, replayed like a graph (same cyclic block
+    order: each replay advances the ring buffer to the block it was prepared for)."""
+
+    def __init__(self, cbuf, block, fn, eng, stream_ptr):
+        self.cbuf, self.block, self.fn, self.eng, self.sp = cbuf, block, fn, eng, stream_ptr
+
+    def replay(self):
+        self.cbuf.carry_over()
+        assert self.cbuf.block == self.block, "prepared chunks must be replayed in cyclic order"
+        self.fn(self.sp)
+        if self.eng.L.mgx_join(self.eng.h, self.sp) != 0:
+            raise RuntimeError("mgx_join failed")
+
+
 def pick_epoch(K, D=512):
     """Refill epoch E (mgx refill_every) so that the K timed steps are whole epochs: the largest
     divisor of K in [8, min(64, D/4)] (at D/2 the ring invariant 2E <= D makes every epoch refill the
@@ -603,15 +628,27 @@ def measure_rollout(args, layout, world, rank, dev):
         else:
             abuf = [actions[W + (c % nchunks) * H:W + (c % nchunks) * H + H].clone() for c in range(ng)]
         s = torch.cuda.Stream(dev)
-        with torch.cuda.stream(s):
+        if args.launch == "eager" and fused and E == H and args.gae_fused:
+            # --launch eager: no graph -- each chunk is ONE prepared C call (mgx_rollout_compact_gae: the epoch's refill
+            # fork, the MT slide, the rollout, the GAE fold) + mgx_join, its ctypes arguments built here once
+            # (CompactBuffer.rollout_launcher); the "graphs" below replay them in the same cyclic block order
+            sp = ctypes.c_void_p(stream.cuda_stream)
             for c in range(ng):
-                gr = torch.cuda.CUDAGraph()
-                gr.capture_begin()
-                chunk(c % nchunks, abuf[c], device_policy=fused)
-                if not fused:                            # this graph's next actions, after its steps read them
-                    random_actions(abuf[c], act_ctr, seed=act_seed)
-                gr.capture_end()
-                graphs.append(gr)
+                cbuf.carry_over()
+                fn = cbuf.rollout_launcher(0, None, K=E, gae=dict(
+                    values=vals, last_values=last_v, gamma=gamma, gae_lambda=lam, out=(adv, ret),
+                    stats=hist[c % nchunks], scratch=scratch))
+                graphs.append(_PreparedChunk(cbuf, cbuf.block, fn, eng, sp))
+        else:
+            with torch.cuda.stream(s):
+                for c in range(ng):
+                    gr = torch.cuda.CUDAGraph()
+                    gr.capture_begin()
+                    chunk(c % nchunks, abuf[c], device_policy=fused)
+                    if not fused:                        # this graph's next actions, after its steps read them
+                        random_actions(abuf[c], act_ctr, seed=act_seed)
+                    gr.capture_end()
+                    graphs.append(gr)
         # one untimed replay of each graph (more warm-up steps: every graph is whole refill epochs
         # ending in a join): the first launch of an instantiated graph pays its upload, ~0.1 ms
         # that a 20-step window would otherwise count as 5 us per step
@@ -838,7 +875,7 @@ def measure_rollout(args, layout, world, rank, dev):
             kstat = _rocprof_kernel_avg(os.path.join(prof_dir, "kernel_stats_%d_%s_e%d.csv" % (
                 args.config, layout, spl if fused else E)), kname)
             t_avg = _rocprof_trace_timed_avg(os.path.join(prof_dir, "kernel_trace_%d_%s_e%d.csv.gz" % (
-                args.config, layout, spl if fused else E)), kname, (W + (ng * H if graphs else 0)) // per, K // per)
+                args.config, layout, spl if fused else E)), kname, steps_since_reset // per, K // per)
             if kstat is not None and t_avg is not None:
                 kstat["timed_avg_us"] = t_avg
         produced = (st1["resets"] - st0["resets"]) + (st1["queued"] - st0["queued"])
@@ -886,7 +923,9 @@ def measure_rollout(args, layout, world, rank, dev):
                            " [compact layout: observation rows into the rollout buffer]" if compact else ""),
                        "problem": args.problem, "mission": mission, "size": args.size, "num_objects": 4,
                        "envs_per_gpu": n, "n_stack": args.n_stack, "parallelism": "env-sharded dp%d" % world,
-                       "hipgraph": bool(graphs), "refill_every": E, "horizon": H, "layout": layout,
+                       "hipgraph": bool(graphs) and not isinstance(graphs[0], _PreparedChunk),
+                       "launch": ("prepared C call per chunk" if graphs and isinstance(graphs[0], _PreparedChunk)
+                                  else "hipGraph per chunk" if graphs else "python per step"), "refill_every": E, "horizon": H, "layout": layout,
                        "host_wait": getattr(args, "host_wait_applied", "auto"),
                        "graph_launch": ("hipGraphLaunch" if args.graph_launch == "raw" else "CUDAGraph.replay")
                        if graphs else None,

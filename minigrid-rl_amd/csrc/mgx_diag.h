@@ -62,6 +62,12 @@
 #ifndef MGX_PUBN_ACQUIRE     // 1: the fused rollout reads ring_pubn with an agent-scope acquire (0: relaxed; A/B of the
 #define MGX_PUBN_ACQUIRE 1   // acquire's cost)
 #endif
+#ifndef MGX_NT_REC           // 1: the refill writes its ring records with non-temporal (streaming) stores (round 6 A/B)
+#define MGX_NT_REC 0
+#endif
+#ifndef MGX_NT_ROWS          // 1: the fused rollout copies its observation rows out with non-temporal stores (round 6 A/B)
+#define MGX_NT_ROWS 0
+#endif
 #ifndef MGX_SERIAL_REFILL   // refill on the caller's stream (the refill alone, for timing it)
 #define MGX_SERIAL_REFILL 0
 #endif

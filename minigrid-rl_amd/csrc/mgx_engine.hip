@@ -168,6 +168,15 @@ struct KParams {
     uint64_t rnd_seed;
 };
 
+// 16-B store, non-temporal (streaming: write-once data the kernel never reads back) when NT
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ void st16(uint4 *p, const uint4 v) {
+    const u32x4_t w = {v.x, v.y, v.z, v.w};      // (one dwordx4 store either way: a HIP uint4 struct copied through a
+    if (NT) __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));   // parameter compiled to four dword stores)
+    else *reinterpret_cast<u32x4_t *>(p) = w;
+}
+
 __device__ __forceinline__ unsigned long long clk_now() { return (unsigned long long)wall_clock64(); }
 __device__ __forceinline__ void clk_record(const KClock &k, int cls, unsigned long long t0) {   // one thread
     unsigned long long *c = k.base[cls];
@@ -1509,7 +1518,7 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
             const int nb16 = (ne * FROW) >> 4;
             const uint4 *src = reinterpret_cast<const uint4 *>(s_stk);
             uint4 *dst = reinterpret_cast<uint4 *>(o.rows + ((int64_t)t_rows * N + e0) * FROW);
-            for (int i = tt; i < nb16; i += nt) dst[i] = src[i];
+            for (int i = tt; i < nb16; i += nt) st16<MGX_NT_ROWS != 0>(dst + i, src[i]);
             const int rem = ((ne * FROW) >> 2) - (nb16 << 2);
             if (tt < rem)
                 reinterpret_cast<uint32_t *>(dst + nb16)[tt] = reinterpret_cast<const uint32_t *>(src + nb16)[tt];
@@ -1993,7 +2002,7 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
                                                                                  16 * (j - GQ));
                 uint4 v = make_uint4(0u, 0u, 0u, 0u);
                 if (j < GQ + 3) v = make_uint4(w[0], w[1], w[2], w[3]);
-                reinterpret_cast<uint4 *>(p.ring_rec + (size_t)ss * (size_t)REC)[j] = v;
+                st16<MGX_NT_REC != 0>(reinterpret_cast<uint4 *>(p.ring_rec + (size_t)ss * (size_t)REC) + j, v);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // (the next round rewrites the stages)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -122,6 +122,13 @@ class CompactBuffer:
         gae: dict(values f32 [K, N], last_values f32 [N], gamma, gae_lambda, out=(adv, ret) f32 [K, N],
         stats=f64 [3] or None, scratch=None) -- also the GAE of these K steps, fused into the launch
         (mgx_rollout_compact_gae): gae_dones(rewards[t:t+K], values, dones of the K steps, ...) bit for bit."""
+        self.rollout_launcher(t, actions, gae, K)()
+
+    def rollout_launcher(self, t, actions, gae=None, K=None):
+        """rollout(t, actions, gae, K) prepared for the CURRENT ring block and not launched: the returned callable
+        issues it with the ctypes arguments built here, once -- one C call per launch (bench.py --launch eager: the
+        timed region's launches without a graph's launch latency).  The tensors it writes are this buffer's; those
+        it reads (actions, GAE inputs) must stay alive and in place."""
         e = self.engine
         if actions is None:
             if getattr(e, "random_policy", None) is None or K is None:
@@ -147,9 +154,10 @@ class CompactBuffer:
         o.ep_return_dev = e.ep_return.data_ptr()
         o.ep_len_dev = e.ep_len.data_ptr()
         o.livelock_dev = e.livelock.data_ptr()
+        ap = _ptr(actions)
+        L, h = e.L, e.h
         if gae is None:
-            _lib.check(e.L.mgx_rollout_compact(e.h, _ptr(actions), K, ctypes.byref(o), e._stream()),
-                       "mgx_rollout_compact")
+            g, keep = None, (actions,)
         else:
             from .engine import _scratch_for
             v, lv = gae["values"], gae["last_values"].reshape(self.N).float().contiguous()
@@ -171,11 +179,21 @@ class CompactBuffer:
             g.adv_stats_dev = stats.data_ptr() if stats is not None else None
             sc = _scratch_for(stats, gae.get("scratch")) if stats is not None else None
             g.stats_scratch_dev = sc.data_ptr() if sc is not None else None
-            _lib.check(e.L.mgx_rollout_compact_gae(e.h, _ptr(actions), K, ctypes.byref(o), ctypes.byref(g),
-                                                   e._stream()), "mgx_rollout_compact_gae")
-        e.calls += K
-        if actions is None:
-            e.random_launches += 1
+            keep = (actions, v, lv, adv, ret, stats, sc)
+        o_ref = ctypes.byref(o)
+        g_ref = ctypes.byref(g) if g is not None else None
+
+        def launch(stream=None):
+            _keep = (o, g, keep)                             # noqa: F841  (the structs and inputs outlive the call)
+            st = stream if stream is not None else e._stream()
+            if g_ref is None:
+                _lib.check(L.mgx_rollout_compact(h, ap, K, o_ref, st), "mgx_rollout_compact")
+            else:
+                _lib.check(L.mgx_rollout_compact_gae(h, ap, K, o_ref, g_ref, st), "mgx_rollout_compact_gae")
+            e.calls += K
+            if actions is None:
+                e.random_launches += 1
+        return launch
 
     def carry_over(self):
         """Start the next rollout: its history rows and observation 0 are this one's last rows (ring: read in

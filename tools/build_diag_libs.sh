@@ -41,6 +41,11 @@ declare -A V=(
   [gskip2]="-DMGX_GEN_SKIP=2"
   [gskip4]="-DMGX_GEN_SKIP=4"
   [gskip32]="-DMGX_GEN_SKIP=32"
+  [ntrec]="-DMGX_NT_REC=1"
+  [ntrows]="-DMGX_NT_ROWS=1"
+  [ntboth]="-DMGX_NT_REC=1 -DMGX_NT_ROWS=1"
+  [sfence0]="-DMGX_SLIDE_FENCE=0"
+  [ntboth_sf0]="-DMGX_NT_REC=1 -DMGX_NT_ROWS=1 -DMGX_SLIDE_FENCE=0"
 )
 names=("$@")
 [ ${#names[@]} -eq 0 ] && names=("${!V[@]}")
