@@ -336,6 +336,8 @@ struct Gen {
     Pcg pcg;
     int ax, ay, adir;
     int goalx, goaly;      // the first Goal added to objs (-1: none): the 'go to goal' target without a scan
+    bool phave;            // gen_multi: this attempt's MT-only prefix comes from prec (a record looked up by the refill)
+    uint64_t prec;
     uint32_t *objs;        // LDS objs list: type | cname<<4 | x<<8 | y<<16 (cname 15 = None)
     int nobjs;
     uint32_t tmask;        // bit t: an object of type t is in objs
@@ -482,8 +484,8 @@ __device__ __forceinline__ int randbelow_c(Gen<NW> &G, const RbConst K) {
     }
 }
 // consume m <= 10 words of the register queue
-template <int NW>
-__device__ __forceinline__ void mt_advance(Gen<NW> &G, int m) {
+template <class GT>
+__device__ __forceinline__ void mt_advance(GT &G, int m) {
     G.cur += (uint64_t)m;
     G.go += m;
     if (G.go >= MT_FIELDS) {
@@ -502,8 +504,8 @@ __device__ __forceinline__ void mt_advance(Gen<NW> &G, int m) {
 // one SWAR compare and a find-first-set each); a draw that finds no accepted word in the rest of the ten
 // consumes them all and continues in the next pass.  Word consumption and the live-lock cap are those of
 // cnt randbelow() calls, which spent a whole pass (and its group rotation) per draw (round 4).
-template <int NW>
-__device__ __forceinline__ uint64_t randbelow_seq(Gen<NW> &G, uint64_t prog, int cnt) {
+template <class GT>
+__device__ __forceinline__ uint64_t randbelow_seq(GT &G, uint64_t prog, int cnt) {
     constexpr uint64_t GM = 32ull * MT_REP;              // guard bit of every slot
     uint64_t res = 0;
     int i = 0;
@@ -870,21 +872,30 @@ __device__ __forceinline__ void key_spec(int nr, int r, int ar, int &kA, int &kB
 
 __device__ const int MULTI_TYPES[3] = {T_KEY, T_BALL, T_BOX};
 
-template <int NW>
-__device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
-    const int S = G.S, mid = S / 2;
-    if (MGX_GEN_SKIP & 8) { G.ax = 1; G.ay = 1; put(G, S - 2, S - 2, CODE_GOAL); add_obj(G, T_GOAL, 15, S - 2, S - 2); return; }
-    for (int i = 1; i < S - 1; i++) put(G, mid, i, CODE_WALL);
-    if (nr == 3) for (int i = 1; i < mid; i++) put(G, i, mid, CODE_WALL);
-    if (nr == 4) for (int i = 1; i < S - 1; i++) put(G, i, mid, CODE_WALL);
-    const int ndoors = nr == 2 ? 1 : nr;
-    const bool ado = G.all_doors_open;
-    uint32_t oc = 0x3FFFFu;    // obj_choice: bit = type_slot*6 + colour-name (key, ball, box)
-    uint32_t dc = 0x3Fu;       // door_colors
-    uint32_t dinfo = 0;        // per door byte: colour | locked<<3 | key_in_box<<4
-    // colour / locked / key_in_box draws, door by door (custom_env.py:635-643, 878-908, 1322-1362):
-    // random.choice(door_colors) of the 6 - d colours left = randbelow(6 - d), locked = choice([True, False])
-    // = randbelow(2) == 0 (not drawn when all_doors_open), key_in_box likewise -- one fixed sequence
+// ---- the MT-only prefix of a multi-room attempt (round 6) -----------------------------------------------------
+// Everything gen_multi / gen_rooms draw before their first PCG64 draw comes from the shared MT19937 stream only:
+// [the mission choice] and randint(2, 4) (custom_env.py:595-615), per door its colour / locked / key_in_box draws
+// (:635-643, 878-908, 1322-1362), per door its position [and is_open] (:646-650, 911-930, 1365-1391).  Every env
+// reads the same stream (quirk Q7), so the prefix is a pure function of the attempt's first word: the MT slide
+// computes it once per stream position (mgx_prefix_kernel, a record per word: KParams.pfx) and the refill looks it
+// up instead of drawing (round-6 measurement: running every prefix sequence twice cost the refill 11 us of 155 per
+// 20-step epoch at config 2 and 55 of 370 per 64-step epoch at config 4).  One function draws it for both.
+struct Prefix {
+    int nr, rc;            // rooms; the mission draw (when the config names no mission)
+    uint32_t dinfo;        // per door byte: colour | locked << 3 | key_in_box << 4
+    uint32_t dpos;         // per door nibble: position - lo (door_geom)
+    uint32_t dopen;        // per door bit: is_open (all_doors_open)
+};
+template <class GT>
+__device__ __forceinline__ void prefix_draws(GT &G, int S, bool draw_cmd, bool ado, Prefix &P) {
+    const uint64_t r = randbelow_seq(G, draw_cmd ? (4ull | (3ull << 5)) : 3ull, draw_cmd ? 2 : 1);
+    P.rc = draw_cmd ? (int)(r & 31) : 0;
+    P.nr = 2 + (int)((draw_cmd ? r >> 5 : r) & 31);
+    P.dinfo = P.dpos = P.dopen = 0;
+    if (G.abort || (MGX_GEN_SKIP & 8)) return;
+    const int nr = P.nr, mid = S / 2, ndoors = nr == 2 ? 1 : nr;
+    // colour / locked / key_in_box: random.choice(door_colors) of the 6 - d colours left = randbelow(6 - d),
+    // locked = choice([True, False]) = randbelow(2) == 0 (not drawn when all_doors_open), key_in_box likewise
     uint64_t prog = 0;
     int cnt = 0;
 #pragma unroll 1
@@ -895,18 +906,16 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     }
     const uint64_t dr = randbelow_seq(G, prog, cnt);
     if (G.abort) return;
+    uint32_t dc = 0x3Fu;       // door_colors
 #pragma unroll 1
     for (int d = 0, k = 0; d < ndoors; d++) {
         const int col = nth_set_bit(dc, (int)(dr >> (5 * k++)) & 31);
         dc &= ~(1u << col);
         const bool lk = ado ? false : ((dr >> (5 * k++)) & 31) == 0;
         const bool kib = ((dr >> (5 * k++)) & 31) == 0;
-        if (lk) { oc &= ~(1u << col); if (kib) oc &= ~(1u << (12 + col)); }
-        dinfo |= (uint32_t)(col | (lk << 3) | (kib << 4)) << (8 * d);
+        P.dinfo |= (uint32_t)(col | (lk << 3) | (kib << 4)) << (8 * d);
     }
-    GSTAMP(G, 11);                                               // walls + door colour/lock draws
-    // door positions (custom_env.py:646-650, 911-930, 1365-1391): randint(lo, hi) = lo + randbelow(hi - lo + 1)
-    // per door [+ is_open = choice([True, False]) when all_doors_open], again one sequence
+    // door positions: randint(lo, hi) = lo + randbelow(hi - lo + 1) per door [+ is_open], again one sequence
     prog = 0;
     cnt = 0;
 #pragma unroll 1
@@ -920,12 +929,60 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
     if (G.abort) return;
 #pragma unroll 1
     for (int d = 0, k = 0; d < ((MGX_GEN_SKIP & 2) ? 0 : ndoors); d++) {
+        P.dpos |= (uint32_t)((pr >> (5 * k++)) & 15) << (4 * d);
+        if (ado) P.dopen |= (uint32_t)(((pr >> (5 * k++)) & 31) == 0) << d;
+    }
+}
+// A prefix record (u64): [0, 8) words the prefix consumed (1..255; 0 = no record), [8, 16) the wrap count of its
+// first word's MT ring slot (stale records of an earlier pass through the ring never match), [16, 18) rooms - 2,
+// [18, 20) the mission draw, then per door 10 bits: colour | locked << 3 | key_in_box << 4 | position << 5 | is_open << 9
+constexpr int PFX_LOOK = 320;       // words past a position its record may read (255 consumed + a 30-word queue)
+__host__ __device__ __forceinline__ uint64_t pfx_pack(const Prefix &P, uint32_t adv, uint32_t tag) {
+    uint64_t r = (uint64_t)(adv & 0xFF) | ((uint64_t)(tag & 0xFF) << 8) | ((uint64_t)(P.nr - 2) << 16) |
+                 ((uint64_t)(P.rc & 3) << 18);
+    for (int d = 0; d < 4; d++)
+        r |= (uint64_t)(((P.dinfo >> (8 * d)) & 31) | (((P.dpos >> (4 * d)) & 15) << 5) | (((P.dopen >> d) & 1) << 9))
+             << (20 + 10 * d);
+    return r;
+}
+__host__ __device__ __forceinline__ void pfx_unpack(uint64_t r, Prefix &P) {
+    P.nr = 2 + (int)((r >> 16) & 3);
+    P.rc = (int)((r >> 18) & 3);
+    P.dinfo = P.dpos = P.dopen = 0;
+    for (int d = 0; d < 4; d++) {
+        const uint32_t f = (uint32_t)(r >> (20 + 10 * d)) & 0x3FFu;
+        P.dinfo |= (f & 31u) << (8 * d);
+        P.dpos |= ((f >> 5) & 15u) << (4 * d);
+        P.dopen |= ((f >> 9) & 1u) << d;
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ void gen_rooms(Gen<NW> &G, const Prefix &P) {
+    const int S = G.S, mid = S / 2, nr = P.nr;
+    if (MGX_GEN_SKIP & 8) { G.ax = 1; G.ay = 1; put(G, S - 2, S - 2, CODE_GOAL); add_obj(G, T_GOAL, 15, S - 2, S - 2); return; }
+    for (int i = 1; i < S - 1; i++) put(G, mid, i, CODE_WALL);
+    if (nr == 3) for (int i = 1; i < mid; i++) put(G, i, mid, CODE_WALL);
+    if (nr == 4) for (int i = 1; i < S - 1; i++) put(G, i, mid, CODE_WALL);
+    const int ndoors = nr == 2 ? 1 : nr;
+    const bool ado = G.all_doors_open;
+    const uint32_t dinfo = P.dinfo;
+    uint32_t oc = 0x3FFFFu;    // obj_choice: bit = type_slot*6 + colour-name (key, ball, box)
+#pragma unroll 1
+    for (int d = 0; d < ndoors; d++) {                           // a locked door's key (or key box) leaves the list
+        const uint32_t di = dinfo >> (8 * d);
+        const int col = di & 7;
+        if ((di >> 3) & 1) { oc &= ~(1u << col); if ((di >> 4) & 1) oc &= ~(1u << (12 + col)); }
+    }
+    GSTAMP(G, 11);                                               // walls + door colour/lock draws
+#pragma unroll 1
+    for (int d = 0; d < ((MGX_GEN_SKIP & 2) ? 0 : ndoors); d++) {
         bool horiz; int lo, hi;
         door_geom(nr, d, mid, S, horiz, lo, hi);
-        const int v = lo + (int)((pr >> (5 * k++)) & 31);
+        const int v = lo + (int)((P.dpos >> (4 * d)) & 15);
         const int x = horiz ? v : mid, y = horiz ? mid : v;
         const uint32_t di = dinfo >> (8 * d);
-        const bool open = ado ? ((pr >> (5 * k++)) & 31) == 0 : false;
+        const bool open = ado && ((P.dopen >> d) & 1);
         put_door(G, x, y, (uint8_t)door_code(di & 7, (di >> 3) & 1, open));
         add_obj(G, T_DOOR, di & 7, x, y);
     }
@@ -1101,15 +1158,23 @@ __device__ __forceinline__ void gen_rooms(Gen<NW> &G, int nr) {
 
 template <int NW>
 __device__ __forceinline__ int gen_multi(Gen<NW> &G) {             // custom_env.py:595-615
-    // [choice([0, 1, 2, 5]) = randbelow(4) when the config names no mission] then randint(2, 4)
+    // [choice([0, 1, 2, 5]) = randbelow(4) when the config names no mission] then randint(2, 4), the doors' draws:
+    // the prefix record the refill looked up for this attempt's first word (G.phave: its words already consumed),
+    // else drawn here
     const bool draw_cmd = G.cfg_mission < 0;
-    const uint64_t r = randbelow_seq(G, draw_cmd ? (4ull | (3ull << 5)) : 3ull, draw_cmd ? 2 : 1);
-    if (G.abort) return 0;
-    const int rc = (int)(r & 31);
-    const int cmd = draw_cmd ? (rc == 3 ? 5 : rc) : G.cfg_mission;
-    const int nr = 2 + (int)((draw_cmd ? r >> 5 : r) & 31);
+    Prefix P;
+    if (G.phave) {
+        pfx_unpack(G.prec, P);
+    } else {
+#if MGX_GEN_PREFIX2   // diagnostic: the prefix drawn twice (the first discarded): its marginal cost
+        { const uint64_t c0_ = G.cur; prefix_draws(G, G.S, draw_cmd, G.all_doors_open != 0, P); G.cur = c0_; G.abort = false; mt_sync(G); }
+#endif
+        prefix_draws(G, G.S, draw_cmd, G.all_doors_open != 0, P);
+        if (G.abort) return 0;
+    }
+    const int cmd = draw_cmd ? (P.rc == 3 ? 5 : P.rc) : G.cfg_mission;
     GSTAMP(G, 10);                                               // mission + room-count draws
-    gen_rooms(G, nr);
+    gen_rooms(G, P);
     return cmd;
 }
 

@@ -29,6 +29,12 @@
 #define MGX_GEN_SKIP 0      // 8 walls + door draws; inside the keys + objects loop 32 the object choice draw;
                             // 64 the refill's mission-token copy into the ring header (SB3 layout's tokens)
 #endif
+#ifndef MGX_GEN_PREFIX2      // run every MT-only prefix draw sequence (mission / room count, door colours, door positions)
+#define MGX_GEN_PREFIX2 0    // twice, the first discarded: an upper bound of what memoising the prefix could save (round 6)
+#endif
+#ifndef MGX_PFX_MEMO         // 1: multi-room refills look the MT-only generator prefix up in per-position records
+#define MGX_PFX_MEMO 1       // (KParams.pfx, round 6); 0: drawn in every attempt (A/B)
+#endif
 #ifndef MGX_DIAG_SKIP       // mgx_step_kernel: skip store classes (2 stack roll, 4 missions, 16 grids)
 #define MGX_DIAG_SKIP 0
 #endif

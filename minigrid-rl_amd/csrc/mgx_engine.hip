@@ -76,6 +76,9 @@ struct MtCtl {
     // that the ceiling alternates between floor and ceil of the target instead of always rounding up
     unsigned long long round_acc;
     int round_cap, round_pad;
+    // prefix records (KParams.pfx): every stream position below rec_done has one (computed by the slide, a pass behind
+    // the stream's generation: positions are read long after they are generated, MT_AHEAD)
+    unsigned long long rec_done;
 };
 constexpr int MT_SB_WORDS = 3120;                         // lcm(624, 10): five MT blocks = 312 whole groups
 constexpr int MT_SB_GROUPS = MT_SB_WORDS / MT_FIELDS;
@@ -166,6 +169,10 @@ struct KParams {
     // rnd_ctr[b] = random-policy launches rollout workgroup b has run (its sole writer); null: off
     unsigned long long *rnd_ctr;
     uint64_t rnd_seed;
+    // multi-room problems with the ring (round 6): the MT-only generator prefix of every stream position, one u64
+    // record per word -- [(group & mt_mask) * 10 + word], mgx_device.h pfx_pack -- or null
+    uint64_t *pfx;
+    int mt_shift;           // log2(ring groups): a position's wrap count is group >> mt_shift
 };
 
 // 16-B store, non-temporal (streaming: write-once data the kernel never reads back) when NT
@@ -343,6 +350,8 @@ __device__ __forceinline__ void load_gen(Gen<NW> &G, const KParams &p, int64_t e
     G.all_doors_open = p.all_doors_open;
     G.n_obstacles = p.n_obstacles;
     G.abort = false;
+    G.phave = false;
+    G.prec = 0;
     G.nobjs = 0;
     G.ax = G.ay = -1;
     G.adir = 0;
@@ -1859,6 +1868,60 @@ __global__ __launch_bounds__(64) void mgx_fixup_kernel(KParams p, KOut o) {
     }
 }
 
+// ========================================================= prefix records
+// The prefix of an attempt that starts at stream word `pos`, decoded straight from the packed ring (no LDS window):
+// the generator's own prefix_draws over a register queue that reads groups from global memory.
+struct PfxQ {
+    const uint64_t *table;
+    uint64_t rmask;
+    uint64_t cur, astart, gi, ga, gb, gc;
+    int go;
+    uint32_t llw, err;
+    bool abort;
+#if MGX_GEN_STAMPS
+    unsigned long long *stamps;
+    uint64_t tlast;
+#endif
+};
+__device__ __forceinline__ uint64_t win_group(PfxQ &Q, uint64_t g) { return Q.table[g & Q.rmask]; }
+__device__ __forceinline__ uint64_t pfx_index(uint64_t pos, uint64_t rmask) {
+    const uint64_t g = div10(pos);
+    return (g & rmask) * MT_FIELDS + (pos - g * MT_FIELDS);
+}
+__device__ __forceinline__ uint32_t pfx_tag(uint64_t pos, int shift) { return (uint32_t)(div10(pos) >> shift) & 0xFFu; }
+// the record for `pos` (0: none -- its prefix would read past the words generated, or takes > 255 of them)
+__device__ __forceinline__ uint64_t pfx_compute(const KParams &p, uint64_t pos) {
+#if MGX_GEN_STAMPS
+    return 0;
+#else
+    PfxQ Q;
+    Q.table = p.mt;
+    Q.rmask = p.mt_mask;
+    Q.cur = Q.astart = pos;
+    const uint64_t g = div10(pos);
+    Q.go = (int)(pos - g * MT_FIELDS);
+    Q.gi = g;
+    Q.ga = win_group(Q, g);
+    Q.gb = win_group(Q, g + 1);
+    Q.gc = win_group(Q, g + 2);
+    Q.llw = p.llw;
+    Q.err = 0;
+    Q.abort = false;
+    Prefix P;
+    prefix_draws(Q, p.S, p.cfg_mission < 0, p.all_doors_open != 0, P);
+    const uint64_t adv = Q.cur - pos;
+    if (Q.abort || adv == 0 || adv > 255) return 0;
+    return pfx_pack(P, (uint32_t)adv, pfx_tag(pos, p.mt_shift));
+#endif
+}
+// records for positions [lo, hi) (mgx_create: the host-generated start of the stream)
+__global__ __launch_bounds__(256) void mgx_prefix_kernel(KParams p, uint64_t lo, uint64_t hi) {
+    for (uint64_t pos = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pos < hi;
+         pos += (uint64_t)gridDim.x * blockDim.x)
+        p.pfx[pfx_index(pos, p.mt_mask)] = pfx_compute(p, pos);
+}
+constexpr int PFX_PER_THREAD = 2;   // records each slide thread computes per launch (4,096 threads at 65,536 envs)
+
 // ============================================================= refill kernel
 // Pre-generates each env's next episodes into its ring until it holds D.
 // Generation is a long serial RNG chain per env (~10^4 dependent ops); doing
@@ -1946,6 +2009,10 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
         // The lane's objs list (dead once its attempt is done) stages the episode's header + RNG snapshot for
         // the wave's record write; its grid is already in LDS (G.g)
         uint32_t *const stg = G.objs;
+        // prefix record of this lane's next attempt, loaded ahead: right after the attempt before it ends (its cursor
+        // is final then), so the load flies during the round's record write
+        uint64_t nrec = 0;
+        if (producer && p.pfx) nrec = p.pfx[pfx_index(G.cur, p.mt_mask)];
         // One attempt per round for every lane: a lane whose attempt live-locked retries while the others
         // already generate their next episode, exactly reset_env's retry semantics per env.  `nfree` budgets
         // ATTEMPTS: an abandoned attempt costs the lane one episode of this epoch's production (unless the
@@ -1961,8 +2028,14 @@ __device__ __forceinline__ void refill_body(const KParams &p) {
                 ResetOut R;
                 G.astart = G.cur;
                 G.abort = false;
+                // a record of this position from the stream's current pass: its words are consumed here, gen_multi
+                // takes its draws from it (the prefix never reaches the live-lock cap: <= 255 of llw words)
+                G.phave = p.pfx && (nrec & 0xFFu) && ((uint32_t)(nrec >> 8) & 0xFFu) == pfx_tag(G.cur, p.mt_shift);
+                G.prec = nrec;
+                if (G.phave) G.cur += nrec & 0xFFu;
                 mt_sync(G);
                 gen_attempt<NW, EXT, MULTI>(G, R);
+                if (p.pfx) nrec = p.pfx[pfx_index(G.cur, p.mt_mask)];
                 if (G.nobjs > p.obj_cap) G.err |= 8u;
                 if (G.abort && ++livelocks <= 100000) {
                     if (nfree > nmin) nfree--;
@@ -2183,6 +2256,19 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
             mx = pc[k] > mx ? pc[k] : mx;
         }
     }
+    // prefix records of the stream positions generated by the slides before this one (round 6): this launch's
+    // threads take PFX_PER_THREAD positions each from rec_done on, up to the last word a record may read
+    unsigned long long rec_lo = 0, rec_hi = 0;
+    if (p.pfx) {
+        rec_lo = c->rec_done;
+        const unsigned long long top = c->hi * (unsigned long long)MT_FIELDS;
+        rec_hi = top > (unsigned long long)PFX_LOOK ? top - PFX_LOOK : 0ull;
+        const unsigned long long T = (unsigned long long)gridDim.x * SLIDE_THREADS;
+        for (int k = 0; k < PFX_PER_THREAD; k++) {
+            const unsigned long long pos = rec_lo + (unsigned long long)blockIdx.x * SLIDE_THREADS + tid + k * T;
+            if (pos < rec_hi) p.pfx[pfx_index(pos, p.mt_mask)] = pfx_compute(p, pos);
+        }
+    }
     // the refill waves' consumption (mgx_refill_kernel writes it in its workgroup stats): one per 64 envs
     unsigned long long cs = 0;
     if (tid < SLIDE_ENVS / 64) {
@@ -2243,6 +2329,10 @@ __global__ __launch_bounds__(SLIDE_THREADS) void mgx_mt_slide_kernel(KParams p) 
             const int r = (int)((acc1 >> 10) - (acc0 >> 10));
             c->round_acc = acc1;
             c->round_cap = r > 1 ? r : 1;
+        }
+        if (p.pfx) {                                  // the positions every workgroup covered (rec_lo, hi as read by all)
+            const unsigned long long T = (unsigned long long)gridDim.x * SLIDE_THREADS * PFX_PER_THREAD;
+            c->rec_done = rec_lo + T < rec_hi ? rec_lo + T : (rec_hi > rec_lo ? rec_hi : rec_lo);
         }
         const unsigned long long m = atomicExch(&c->span_min, ~0ull);   // every workgroup's extremes; reset
         const unsigned long long x = atomicExch(&c->span_max, 0ull);
@@ -2736,7 +2826,7 @@ struct mgx_handle {
                             // (round 2: the all-problems kernel measured the same speed)
     hipStream_t side;       // refill stream
     hipEvent_t ev_fork, ev_done;
-    void *allocs[18];       // [17]: mgx_set_random_policy's per-workgroup launch counters
+    void *allocs[19];       // [17]: mgx_set_random_policy's per-workgroup launch counters, [18] prefix records
     uint32_t *scene_dev;    // mgx_scene's record (inside allocs[15], inline mode only)
 };
 
@@ -3020,6 +3110,9 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     p.start_rng = nullptr;
     p.rnd_ctr = nullptr;                   // random policy off (mgx_set_random_policy)
     p.rnd_seed = 0;
+    p.pfx = nullptr;                       // prefix records: multi-room problems with the ring (below)
+    p.mt_shift = 0;
+    while ((1ll << p.mt_shift) < ring_groups) p.mt_shift++;
     if (D == 0) {   // inline mode: keep each episode's generation start state (mgx_scene) + its record
         const size_t bytes = (size_t)N * 32 + MGX_SCENE_WORDS * sizeof(uint32_t);
         hipError_t e = hipMalloc(&h->allocs[15], bytes);
@@ -3099,6 +3192,27 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming);
         if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "side stream / events"));
+    }
+    if (MGX_PFX_MEMO && cfg->problem == MGX_PROBLEM_MULTI && D > 0) {
+        // prefix records (round 6): one u64 per word of the MT ring (671 MB at the default 2^26-word ring), zeroed (no
+        // record), then the records of the host-generated start of the stream; the slides keep them a pass behind
+        const size_t words = (size_t)ring_groups * MT_FIELDS;
+        hipError_t e = hipMalloc(&h->allocs[18], words * sizeof(uint64_t));
+        if (e != hipSuccess) return bail(fail(MGX_ERR_OOM, "hipMalloc prefix records"));
+        e = hipMemset(h->allocs[18], 0, words * sizeof(uint64_t));
+        if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "hipMemset prefix records"));
+        p.pfx = (uint64_t *)h->allocs[18];
+        const long long top = hi0 * MT_FIELDS - PFX_LOOK;
+        if (top > 0) {
+            hipLaunchKernelGGL(mgx_prefix_kernel, dim3(1024), dim3(256), 0, 0, p, 0ull, (unsigned long long)top);
+            e = hipGetLastError();
+            if (e == hipSuccess) {
+                const unsigned long long rd = (unsigned long long)top;
+                e = hipMemcpy((char *)h->allocs[16] + offsetof(MtCtl, rec_done), &rd, sizeof rd, hipMemcpyHostToDevice);
+            }
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+            if (e != hipSuccess) return bail(fail(MGX_ERR_HIP, "prefix records"));
+        }
     }
     (void)hipSetDevice(prev);
     *out = h;

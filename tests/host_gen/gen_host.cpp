@@ -88,6 +88,7 @@ int run(int problem, int mission, int S, int nobj, int ado, int n_obst, int n, i
         G.problem = problem; G.cfg_mission = mission; G.num_objects = nobj; G.all_doors_open = ado;
         G.n_obstacles = n_obst;
         G.abort = false; G.nobjs = 0; G.ax = G.ay = -1; G.adir = 0;
+        G.phave = false; G.prec = 0;                       // no prefix records on the host: every prefix drawn
         gen_init(G);
         pcg_seed(G.pcg, (uint64_t)(seed + i));
         G.cur = 0;

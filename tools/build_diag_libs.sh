@@ -41,6 +41,8 @@ declare -A V=(
   [gskip2]="-DMGX_GEN_SKIP=2"
   [gskip4]="-DMGX_GEN_SKIP=4"
   [gskip32]="-DMGX_GEN_SKIP=32"
+  [prefix2]="-DMGX_GEN_PREFIX2=1"
+  [nomemo]="-DMGX_PFX_MEMO=0"
   [ntrec]="-DMGX_NT_REC=1"
   [ntrows]="-DMGX_NT_ROWS=1"
   [ntboth]="-DMGX_NT_REC=1 -DMGX_NT_ROWS=1"
