@@ -8,12 +8,13 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/dp
 mkdir -p $O
 for np in 2 4; do
-  MGX_DIST_BACKEND=gloo timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 --master-port $((29500 + np)) bench.py --gpus $np --steps 64 --warmup 5 --cpu-seconds 0 > $O/dp$np.json 2>$O/dp$np.err || { tail -20 $O/dp$np.err; exit 1; }
+  MGX_DIST_BACKEND=gloo timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 --master-port $((29500 + np)) bench.py --gpus $np --steps ${STEPS:-20} --warmup 5 --cpu-seconds 0 > $O/dp$np.json 2>$O/dp$np.err || { tail -20 $O/dp$np.err; exit 1; }
   # gloo prints its connection banner on stdout (RCCL does not): keep the bench's JSON line only
   grep '^{"metric"' $O/dp$np.json > $O/dp$np.line.json
   python -c "
 import json; d=json.load(open('$O/dp$np.line.json'))
-print('np $np n_gpus', d['n_gpus'], 'ranks_seen', d['ranks_seen'], 'backend', d['dist_backend'], 'value %.3e' % d['value'], d['config']['timed'])"
+s = d.get('steady_state') or {}
+print('np $np n_gpus', d['n_gpus'], 'ranks_seen', d['ranks_seen'], 'backend', d['dist_backend'], 'value %.3e' % d['value'], 'steady %.3e' % s.get('value', 0), 'after', d.get('steps_after_reset'), d['config']['timed'])"
 done
 # the PPO workload (BASELINE config 3's loop) at 2 ranks: gradient + adv-stat all-reduces over gloo, each rank
 # its own 16,384-env shard
