@@ -55,9 +55,9 @@
 #ifndef MGX_ROLL_EPB_S16     // envs per fused-rollout block at S = 16 (config 5): 64, or 32 (twice the blocks, half the LDS;
 #define MGX_ROLL_EPB_S16 32  // round 5 A/B, 2 rotating rounds: config 5 5.13-5.16 vs 5.05-5.06 x 10^9, kernel 24.4-24.6 vs
 #endif                      // 24.9 us per step)
-#ifndef MGX_ROLL_LOGIC_PRIO  // fused rollout: s_setprio of wave 0 during its step logic (0: none; the block waits for it)
-#define MGX_ROLL_LOGIC_PRIO 0
-#endif
+#ifndef MGX_ROLL_LOGIC_PRIO  // fused rollout: s_setprio of wave 0 during its step logic (0: none; the block waits for it).
+#define MGX_ROLL_LOGIC_PRIO 3  // Round 6 A/B (3 rotating rounds, prefix records in: refill and rollout balanced): driver's line
+#endif                        // 6.76-7.01 vs 6.70-6.83 x 10^9, default line 9.23 vs 8.46, config 4 6.03 vs 6.16 (round 5: neutral)
 #ifndef MGX_SLIDE_FENCE      // 1: the MT slide orders its reductions with __threadfence() (an L2 write-back per workgroup),
 #define MGX_SLIDE_FENCE 1    // 0: by waiting for its returning atomics.  Round 5 A/B (rotating order, 3 + 2 rounds): the
 #endif                      // fenced slide is the faster pipeline -- 20-step line 5.88 vs 5.71, default line 7.97-8.07 vs 7.35

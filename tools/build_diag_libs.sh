@@ -43,6 +43,7 @@ declare -A V=(
   [gskip32]="-DMGX_GEN_SKIP=32"
   [prefix2]="-DMGX_GEN_PREFIX2=1"
   [nomemo]="-DMGX_PFX_MEMO=0"
+  [lp3p1]="-DMGX_ROLL_LOGIC_PRIO=3 -DMGX_REFILL_PRIO=1"
   [ntrec]="-DMGX_NT_REC=1"
   [ntrows]="-DMGX_NT_ROWS=1"
   [ntboth]="-DMGX_NT_REC=1 -DMGX_NT_ROWS=1"
