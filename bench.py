@@ -673,7 +673,8 @@ def measure_rollout(args, layout, world, rank, dev):
     # graphs, replayed once each; eagerly, counted as they run)
     forks = (st0["refill_launches"] - forks0) * nchunks // len(graphs) if graphs else None
     hist.zero_()                                         # (the untimed replays accumulated into it)
-    clk0 = (eng.clock_launches(0), eng.clock_launches(1), eng.clock_launches(2))   # launch counts at the region's start
+    scls = eng.rollout_clock_class() if fused else 0     # (S = 16 fused: the 32-env blocks' own class)
+    clk0 = (eng.clock_launches(scls), eng.clock_launches(1), eng.clock_launches(2))   # launch counts at the region's start
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -708,8 +709,8 @@ def measure_rollout(args, layout, world, rank, dev):
         torch.cuda._sleep(1000)                          # trace marker: the region ended
         torch.cuda.synchronize(dev)
     gpu_ms = ev0.elapsed_time(ev1)
-    clk1 = (eng.clock_launches(0), eng.clock_launches(1), eng.clock_launches(2))
-    timed_step_us = eng.clock_spans_us(0, clk0[0], clk1[0])      # the timed region's own kernel launches
+    clk1 = (eng.clock_launches(scls), eng.clock_launches(1), eng.clock_launches(2))
+    timed_step_us = eng.clock_spans_us(scls, clk0[0], clk1[0])   # the timed region's own kernel launches
     timed_refill_us = eng.clock_spans_us(1, clk0[1], clk1[1])
     timed_slide_us = eng.clock_spans_us(2, clk0[2], clk1[2])
     st1 = eng.stats()

@@ -308,7 +308,9 @@ mgx_status mgx_scene(mgx_handle *h, int64_t env, uint32_t *record, void *stream)
  * far, per workgroup), then rec u64 [slots][G][2] {start, end} of launches 0 .. slots-1 (later
  * launches are counted, not recorded).  Kernel parameters are captured at launch: set the clock
  * before capturing a graph.  NULL clock_dev: off (the default). */
-#define MGX_CLOCK_CLASSES 3   /* 0 step kernels, 1 refill, 2 MT slide (the kernel that follows each refill) */
+#define MGX_CLOCK_CLASSES 4   /* 0 step kernels (64-env blocks), 1 refill, 2 MT slide (the kernel that follows each
+                                 refill), 3 (ABI 7) the fused rollout's 32-env blocks at S = 16 (0 groups otherwise):
+                                 every launch of a class has its class's grid */
 int64_t mgx_clock_words(const mgx_handle *h, int slots);
 int mgx_clock_groups(const mgx_handle *h, int cls);
 mgx_status mgx_set_clock(mgx_handle *h, uint64_t *clock_dev, int slots, int *tick_khz);

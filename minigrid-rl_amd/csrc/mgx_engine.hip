@@ -99,7 +99,9 @@ __host__ __device__ constexpr int scratch_per_env(int obj_stride, int nw) { retu
 // same grid) and of its record of launch cnt[b] -- plain stores, one 16-B record per workgroup (a first version
 // reduced with device-scope atomics on one address per launch and cost the 1,024-workgroup step kernel 48 us).
 // Class block (u64): cnt[G], then [slots][G] records {start, end}; G = the class's grid (mgx_clock_groups).
-enum { CLK_STEP = 0, CLK_REFILL = 1, CLK_SLIDE = 2, CLK_CLASSES = 3 };
+// class 3 (round 6): the fused rollout's 32-env blocks (S = 16), whose grid is twice the step kernels' --
+// every launch of a class must have the class's grid (workgroup b counts the launches it took part in)
+enum { CLK_STEP = 0, CLK_REFILL = 1, CLK_SLIDE = 2, CLK_ROLL32 = 3, CLK_CLASSES = 4 };
 struct KClock {
     unsigned long long *base[CLK_CLASSES];   // per class: cnt[G] then rec[slots][G][2]
     int groups[CLK_CLASSES];
@@ -1798,7 +1800,7 @@ __global__ __launch_bounds__(4 * EPB + 64, 4) void mgx_rollout_kernel(KParams p,
     }
     if (p.clk.slots) {                            // every wave of the workgroup is done
         __syncthreads();
-        if (tid == 0) clk_record(p.clk, CLK_STEP, s_t0);
+        if (tid == 0) clk_record(p.clk, EPB == 32 ? CLK_ROLL32 : CLK_STEP, s_t0);
     }
 }
 
@@ -3404,7 +3406,8 @@ mgx_status mgx_set_seed(mgx_handle *h, int64_t seed) {
 // grid of every launch of a clocked kernel class (the clock's per-workgroup records need one grid per class)
 static int clock_groups(const mgx_handle *h, int cls) {
     const int64_t nblk = (h->kp.n + BLOCK_ENVS - 1) / BLOCK_ENVS;
-    if (cls == CLK_STEP) return (int)std::max<int64_t>(nblk, (h->kp.n + h->roll_epb - 1) / h->roll_epb);
+    if (cls == CLK_STEP) return (int)nblk;
+    if (cls == CLK_ROLL32) return h->roll_epb == 32 && h->kp.S == 16 ? (int)((h->kp.n + 31) / 32) : 0;
     if (cls == CLK_SLIDE) return (int)((h->kp.n + SLIDE_ENVS - 1) / SLIDE_ENVS);
     return (int)((h->kp.n + h->kp.refill_epw - 1) / h->kp.refill_epw);   // (64 except the S = 8 kernel's 32/16)
 }

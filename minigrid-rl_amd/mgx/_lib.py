@@ -28,7 +28,7 @@ EXPORTS = ("mgx_last_error", "mgx_abi_version", "mgx_create", "mgx_destroy", "mg
            "mgx_step_compact", "mgx_rollout_compact", "mgx_rollout_compact_gae", "mgx_observe_compact", "mgx_gather",
            "mgx_gather_ring", "mgx_scene", "mgx_set_clock", "mgx_clock_words", "mgx_clock_groups",
            "mgx_ring_levels", "mgx_random_actions", "mgx_set_random_policy")
-CLOCK_CLASSES = 3   # == MGX_CLOCK_CLASSES (include/mgx.h)
+CLOCK_CLASSES = 4   # == MGX_CLOCK_CLASSES (include/mgx.h)
 
 
 class MgxConfig(ctypes.Structure):

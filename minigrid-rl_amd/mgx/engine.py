@@ -186,7 +186,13 @@ class MgxEngine:
     def clock_launches(self, cls=0):
         """Launches of kernel class `cls` so far (synchronises)."""
         torch.cuda.synchronize(self.device)
-        return int(self.clock[self._clock_blocks[cls][0]])
+        off, g = self._clock_blocks[cls]
+        return int(self.clock[off]) if g > 0 else 0
+
+    def rollout_clock_class(self):
+        """The clock class of this engine's fused rollout launches: 3 for the 32-env blocks at S = 16, else 0 (the
+        step kernels' class; include/mgx.h MGX_CLOCK_CLASSES)."""
+        return 3 if self._clock_blocks[3][1] > 0 else 0
 
     def clock_spans_us(self, cls, first, last):
         """Durations (us) of launches [first, last) of kernel class `cls`: min workgroup start to max workgroup

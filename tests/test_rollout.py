@@ -399,3 +399,32 @@ def test_kernel_clock_records_every_launch():
     sa, sb = a.dump_state(), b.dump_state()
     for k in ("grid", "agent", "mtwords", "pcg"):
         assert np.array_equal(sa[k], sb[k]), k
+
+
+@pytest.mark.gpu
+def test_kernel_clock_classes_keep_their_grids_at_s16():
+    """at S = 16 the fused rollout runs 32-env blocks (twice the step kernels' grid); it records into a clock
+    class of its own (3), so per-step launches (class 0) and rollout launches on one engine never mix grids."""
+    _need_gpu()
+    from mgx import MgxEngine
+    from mgx.compact import CompactBuffer
+    n, E = 1024, 8
+    eng = MgxEngine(problem="multi", mission=1, size=16, n_envs=n, refill_every=E, mission_dtype=torch.uint8)
+    eng.enable_clock(slots=16)
+    assert eng.rollout_clock_class() == 3
+    cb = CompactBuffer(eng, E, ring=True)
+    eng.reset()
+    cb.observe(0)
+    acts = torch.randint(0, 7, (3 * E, n), device=eng.device, dtype=torch.int32)
+    cb.rollout(0, acts[:E])
+    for t in range(E):
+        cb.step(t, acts[E + t])
+    cb.carry_over()
+    cb.rollout(0, acts[2 * E:])
+    eng.join()
+    torch.cuda.synchronize()
+    assert eng.clock_launches(0) == E and eng.clock_launches(3) == 2
+    for cls, k in ((0, E), (3, 2)):
+        spans = eng.clock_spans_us(cls, 0, k)
+        assert len(spans) == k and all(0 < x < 1e5 for x in spans), (cls, spans)
+    eng.poll_error()

@@ -81,7 +81,7 @@ for w in range(windows):
     s1 = eng.stats()
     steps += per_window * E
     refill = eng.clock_spans_us(1, 0, per_window)
-    roll = eng.clock_spans_us(0, 0, per_window)
+    roll = eng.clock_spans_us(eng.rollout_clock_class(), 0, per_window)
     lv = eng.ring_levels().astype(np.int64)
     cons = s1["resets"] - s0["resets"]
     prod = cons + s1["queued"] - s0["queued"]
