@@ -217,7 +217,8 @@ def test_frame_stack_and_terminal_obs_match_sb3_layer(name, n_stack, mdt):
 
 @pytest.mark.parametrize("problem,mission,size,ado", [("multi", 5, 8, 0), ("multi", None, 8, 0), ("multi", 2, 8, 0),
                                                       ("multi", None, 16, 0), ("multi", 1, 16, 0), ("gto", None, 8, 0),
-                                                      ("multi", None, 8, 1), ("multi", 1, 16, 1)])
+                                                      ("multi", None, 8, 1), ("multi", 1, 16, 1),
+                                                      ("multi", None, 11, 0)])   # (testing.yaml's size: the 11x11 evals)
 def test_engine_matches_oracle_1024_envs(problem, mission, size, ado):
     """Bit-exact transitions vs the C oracle at 1,024 envs x 256 random steps
     (global env index offset 4096 exercises sharded seeding).  ado: all_doors_open=True
