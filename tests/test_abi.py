@@ -75,3 +75,14 @@ def test_mission_text_table(lib):
     assert _lib.mission_text(1 | (3 << 2) | (0 << 5)) == "toggle purple door"
     assert _lib.mission_text(128) == "drop"
     assert [_lib.mission_text(129 + d) for d in range(4)] == ["move left", "move right", "move up", "move down"]
+
+
+def test_random_actions_rejects_bad_arguments_without_gpu(lib):
+    """mgx_random_actions (ABI 7) refuses an empty batch, a null buffer / counter and n_actions outside
+    [1, 65536] with MGX_ERR_INVALID before any HIP call."""
+    dummy = ctypes.c_void_p(0x1000)                     # never dereferenced: the checks come first
+    for out, count, na, ctr in [(dummy, 0, 7, dummy), (dummy, -5, 7, dummy), (None, 16, 7, dummy),
+                                (dummy, 16, 7, None), (dummy, 16, 0, dummy), (dummy, 16, 65537, dummy)]:
+        st = lib.mgx_random_actions(out, count, na, ctypes.c_uint64(1), ctr, None)
+        assert st == 1, (count, na, st)                  # MGX_ERR_INVALID
+        assert b"mgx_random_actions" in lib.mgx_last_error()

@@ -45,6 +45,22 @@ def test_random_actions_match_reference_and_advance():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_actions", [1, 2, 65536])
+def test_random_actions_extreme_action_counts(n_actions):
+    """n_actions at the ABI's bounds: 1 (every draw 0), 2, and 65,536 -- equal to the host restatement."""
+    from mgx import random_actions
+    dev = torch.device("cuda", 0)
+    out = torch.empty(4097, dtype=torch.int32, device=dev)
+    ctr = torch.zeros(2, dtype=torch.int64, device=dev)
+    random_actions(out, ctr, seed=2024, n_actions=n_actions)
+    got = out.cpu().numpy()
+    assert np.array_equal(got, O.random_actions_ref(4097, 2024, 0, n_actions=n_actions))
+    assert got.min() >= 0 and got.max() < n_actions
+    if n_actions == 1:
+        assert not got.any()
+
+
+@pytest.mark.gpu
 def test_random_actions_fresh_in_graph_replays():
     from mgx import random_actions
     dev = torch.device("cuda", 0)
