@@ -74,6 +74,9 @@
 #ifndef MGX_NT_ROWS          // 1: the fused rollout copies its observation rows out with non-temporal stores (round 6 A/B)
 #define MGX_NT_ROWS 0
 #endif
+#ifndef MGX_ROLL_LDS_PAD     // diagnostic: extra dynamic LDS bytes per fused-rollout workgroup (fewer workgroups per CU:
+#define MGX_ROLL_LDS_PAD 0   // the residency's share of the rollout's time, round 6)
+#endif
 #ifndef MGX_SERIAL_REFILL   // refill on the caller's stream (the refill alone, for timing it)
 #define MGX_SERIAL_REFILL 0
 #endif

@@ -3145,7 +3145,8 @@ mgx_status mgx_create(const mgx_config *cfg, int device, mgx_handle **out) {
     // [+ 'move' target ranges]
     const auto roll_lds = [&](int epb) {
         return (size_t)((epb * FROW + 15) & ~15) + (size_t)epb * 3 * GS + (size_t)epb * 2 * 16 + (size_t)2 * epb * 4 +
-               ((cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL) ? (size_t)epb * 8 : 0);
+               ((cfg->problem == MGX_PROBLEM_MOV || cfg->problem == MGX_PROBLEM_FULL) ? (size_t)epb * 8 : 0) +
+               (size_t)MGX_ROLL_LDS_PAD;
     };
     h->lds_rollout = roll_lds(64);
     h->lds_rollout32 = roll_lds(32);

@@ -49,6 +49,9 @@ declare -A V=(
   [ntboth]="-DMGX_NT_REC=1 -DMGX_NT_ROWS=1"
   [sfence0]="-DMGX_SLIDE_FENCE=0"
   [ntboth_sf0]="-DMGX_NT_REC=1 -DMGX_NT_ROWS=1 -DMGX_SLIDE_FENCE=0"
+  [serial_pad4]="-DMGX_SERIAL_REFILL=1 -DMGX_ROLL_LDS_PAD=6000"
+  [serial_pad3]="-DMGX_SERIAL_REFILL=1 -DMGX_ROLL_LDS_PAD=13500"
+  [pad4]="-DMGX_ROLL_LDS_PAD=6000"
 )
 names=("$@")
 [ ${#names[@]} -eq 0 ] && names=("${!V[@]}")
